@@ -1,0 +1,176 @@
+/*
+ * pbr_shade.h -- C ABI of the MI355X (gfx950) G-buffer shading library, libpbrshade.so.
+ *
+ * Drop-in for the hot path of trevordblack/Physically_Based_Renderer: the per-pixel Cook-Torrance
+ * pixel shader PS (Source/Shaders/Default.hlsl:47-161) and everything it calls in
+ * Source/Shaders/LightingUtil.hlsl:35-225, which the reference runs by DrawIndexedInstanced
+ * (Source/App/PBRApp.cpp:1133) inside PBRApp::Draw (PBRApp.cpp:245-352). The D3D12 rasteriser
+ * front-end is replaced by a flat structure-of-arrays G-buffer the caller fills (pbr_gbuffer_fill
+ * below does it on the host for the benchmark scenes).
+ *
+ * Conventions (mirroring the reference's HRESULT/ThrowIfFailed checking, d3dUtil.h:156-163):
+ *   - every function returns int: 0 = PBR_OK, negative = pbr_status; no exception crosses the ABI;
+ *   - the caller owns every buffer passed in; the library never frees them;
+ *   - device work is stream-ordered and asynchronous on the hipStream_t given (NULL = default
+ *     stream); a context is bound to one device and may be used from several streams, but calls
+ *     that change its state (pbr_set_pass, pbr_set_env_map) are ordered only on their own stream.
+ * Plain C types only (hipStream_t is passed as void*).
+ */
+#ifndef PBR_SHADE_H
+#define PBR_SHADE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBR_ABI_VERSION 1
+#define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
+
+typedef enum pbr_status {
+    PBR_OK = 0,
+    PBR_ERR_INVALID_ARGUMENT = -1,
+    PBR_ERR_NO_DEVICE = -2,
+    PBR_ERR_OUT_OF_MEMORY = -3,
+    PBR_ERR_LAUNCH = -4,
+    PBR_ERR_HIP = -5,
+    PBR_ERR_NOT_READY = -6, /* shade called before pbr_set_pass / IBL without pbr_set_env_map */
+    PBR_ERR_UNSUPPORTED = -7
+} pbr_status;
+
+/* One light, byte-identical to the reference cbuffer element `Light` (LightingUtil.hlsl:9-17,
+ * C++ mirror d3dUtil.h:144-152): 48 bytes, float4-aligned. Lights of a pass are ordered
+ * directional [0, n_dir), point [n_dir, n_dir+n_point), spot [.., +n_spot) as ComputeLighting
+ * expects (LightingUtil.hlsl:176-199). */
+typedef struct pbr_light {
+    float strength[3];
+    float spot_power;   /* spot only */
+    float direction[3]; /* directional / spot only */
+    float pad0;
+    float position[3];  /* point / spot only */
+    float pad1;
+} pbr_light;
+
+typedef enum pbr_ambient_mode {
+    PBR_AMBIENT_CONSTANT = 0,   /* g_AmbientLight * albedo: the active reference code, Default.hlsl:150 */
+    PBR_AMBIENT_IBL_DIFFUSE = 1 /* the diffuse-IBL block of Default.hlsl:140-149 (commented out there) */
+} pbr_ambient_mode;
+
+enum pbr_pass_flags {
+    PBR_FLAG_F0_PLANE = 1u << 0,    /* F0 from the G-buffer (SPECULAR_TEXTURE permutation, Default.hlsl:91-92);
+                                       otherwise F0 = lerp(fresnel_r0, albedo, metallic) (Default.hlsl:94-95) */
+    PBR_FLAG_APPLY_AO = 1u << 1,    /* extension: ambient *= AO. The reference never reads its AO slot. */
+    PBR_FLAG_TILED_CULLING = 1u << 2 /* per-tile range culling of point/spot lights; output is
+                                        bit-identical to the unculled pass ("exact culling") */
+};
+
+/* Per-frame constants: the shading subset of cbPass (Core.hlsl:35-61, FrameResource.h:19-44) and
+ * cbMaterial (Core.hlsl:64-81, Material.h:10-29). */
+typedef struct pbr_pass_desc {
+    float eye_pos_w[3];     /* g_CameraPosW */
+    float ambient_light[3]; /* g_AmbientLight.rgb */
+    float fresnel_r0[3];    /* g_FresnelR0 (default 0.04) */
+    float opacity;          /* g_Opacity -> output alpha (default 1) */
+    int32_t num_dir_lights;   /* NUM_DIR_LIGHTS   (Core.hlsl:1-3)  */
+    int32_t num_point_lights; /* NUM_POINT_LIGHTS (Core.hlsl:5-7)  */
+    int32_t num_spot_lights;  /* NUM_SPOT_LIGHTS  (Core.hlsl:9-11) */
+    int32_t ambient_mode;     /* pbr_ambient_mode */
+    uint32_t flags;           /* pbr_pass_flags */
+    const pbr_light* lights;  /* HOST pointer, num_dir+num_point+num_spot lights */
+} pbr_pass_desc;
+
+/* Structure-of-arrays G-buffer in DEVICE memory: one fp32 plane per channel, `row_stride`
+ * elements between rows. Replaces the interpolated VertexOut + texture fetches of PS
+ * (Default.hlsl:12-20, 79-116): N is the final (normal-mapped) normal, F0 optional. */
+typedef struct pbr_gbuffer_soa {
+    const float* pos_w[3];    /* PosW x, y, z */
+    const float* normal_w[3]; /* N x, y, z */
+    const float* albedo[3];   /* diffuseAlbedo r, g, b */
+    const float* metallic;
+    const float* roughness;
+    const float* ao;          /* read only with PBR_FLAG_APPLY_AO; may be NULL otherwise */
+    const float* f0[3];       /* read only with PBR_FLAG_F0_PLANE; may be NULL otherwise */
+    int32_t width;
+    int32_t height;
+    int64_t row_stride;       /* elements; >= width */
+} pbr_gbuffer_soa;
+
+typedef struct pbr_context pbr_context;
+
+/* Replaces device creation + root signature / PSO build (d3dApp.cpp:437-501, PBRApp.cpp:607-650,
+ * 776-881). `device` is a HIP device ordinal. */
+int pbr_context_create(int device, pbr_context** out_ctx);
+int pbr_context_destroy(pbr_context* ctx);
+
+/* Replaces UpdateMainPassCB + UploadBuffer::CopyData (PBRApp.cpp:455-502, UploadBuffer.h:53):
+ * uploads the light list and constants, stream-ordered; `pass` may be reused on return. */
+int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream);
+
+/* Replaces loading + binding the environment SRV (PBRApp.cpp:1205-1210, t0-t1): an R16G16B16A16_UNORM
+ * texture, `texels` = HOST pointer to width*height*4 u16, row-major. Sampled with linear-wrap
+ * filtering (g_SamLinearWrap, PBRApp.cpp:1157-1162) by the IBL_DIFFUSE ambient. */
+int pbr_set_env_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int32_t height, void* stream);
+
+/* Replaces DrawIndexedInstanced(PS) (PBRApp.cpp:1133, Default.hlsl:47-161): shades every pixel of
+ * `gb` with the current pass into `out_rgba` (DEVICE, fp32 RGBA, out_row_stride PIXELS between rows).
+ * Asynchronous on `stream`. Pixels are independent, so a caller can shade a row band by offsetting
+ * the plane pointers (multi-GPU row tiles). */
+int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rgba, int64_t out_row_stride,
+                      void* stream);
+
+/* Tiled-culling statistics of the last culled pass on `stream` (synchronises that stream):
+ * total surviving point/spot lights summed over tiles, and the tile count. */
+int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream);
+
+/* ---- Host G-buffer fill (replaces the VS + rasteriser front-end, Default.hlsl:22-45) ---------- */
+
+typedef enum pbr_scene_kind {
+    PBR_SCENE_SPHERE_RUSTEDIRON = 1, /* BASELINE config 1: ray-cast unit sphere, rustediron metal/rough */
+    PBR_SCENE_RANDOM_COVERED = 2,    /* configs 2, 3, 5: fully covered synthetic G-buffer */
+    PBR_SCENE_PLANE_MATERIALS = 4    /* config 4: plane y = 0 seen top-down, seven *_1K material sets */
+} pbr_scene_kind;
+
+/* Host-side texture tiles the scenes sample (owned by the caller). */
+typedef struct pbr_scene_assets {
+    const uint8_t* rust_metallic;  /* rust_size^2 u8 gray */
+    const uint8_t* rust_roughness; /* rust_size^2 u8 gray */
+    int32_t rust_size;
+    const uint8_t* mat_albedo;     /* [num_materials][mat_size][mat_size][3] */
+    const uint8_t* mat_specular;   /* [num_materials][mat_size][mat_size][3] */
+    const uint8_t* mat_roughness;  /* [num_materials][mat_size][mat_size]    */
+    const uint8_t* mat_metallic;   /* [num_materials][mat_size][mat_size]    */
+    const uint8_t* mat_has_metallic; /* [num_materials] */
+    const uint8_t* mat_normal;     /* [num_materials][mat_size][mat_size][3] */
+    int32_t num_materials;
+    int32_t mat_size;
+} pbr_scene_assets;
+
+typedef struct pbr_scene_desc {
+    int32_t kind;         /* pbr_scene_kind */
+    int32_t width;        /* full-frame size: pixel values depend on the global (x, y) only, */
+    int32_t height;       /* never on how rows are partitioned across calls or ranks */
+    uint64_t seed;
+    const pbr_scene_assets* assets;
+} pbr_scene_desc;
+
+/* Fills rows [row_begin, row_end) of the full frame into HOST planes laid out like
+ * pbr_gbuffer_soa (15 planes in the order pos xyz, normal xyz, albedo rgb, metallic, roughness,
+ * ao, f0 rgb; `planes[i]` points at row `row_begin`; `row_stride` elements). Returns the number of
+ * covered (non-background) pixels, or a negative pbr_status. */
+int64_t pbr_gbuffer_fill(const pbr_scene_desc* scene, int32_t row_begin, int32_t row_end, float* const* planes,
+                         int64_t row_stride, int32_t n_threads);
+
+/* The light list and pass constants of a benchmark scene (`n_lights` point lights; kind 1 uses one
+ * light at (20, 20, -20), strength 100, PBRApp.cpp:490-491). `pass->lights` is set to `lights`. */
+int pbr_scene_pass(const pbr_scene_desc* scene, int32_t n_lights, pbr_light* lights, pbr_pass_desc* pass);
+
+const char* pbr_strerror(int status);
+/* Last HIP error string recorded by the context (empty if none). */
+const char* pbr_last_error(const pbr_context* ctx);
+int pbr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBR_SHADE_H */

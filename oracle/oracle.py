@@ -1,0 +1,161 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY (ctypes front for the parity checker).
+
+Loads ``oracle/liboracle.so`` (plain-C restatement, pbr_oracle.c) or ``oracle/_ref/libpbr_ref.so``
+(the reference's own LightingUtil.hlsl compiled as C++, ref_harness.cpp). Only tests/,
+``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg may import this module; the product
+package never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libpbr_ref.so")
+REFERENCE_SHADER = "/root/reference/Source/Shaders/LightingUtil.hlsl"
+
+NUM_PLANES = 15
+PLANE_NAMES = ("px", "py", "pz", "nx", "ny", "nz", "ar", "ag", "ab",
+               "metal", "rough", "ao", "f0r", "f0g", "f0b")
+AMBIENT_CONSTANT = 0
+AMBIENT_IBL_DIFFUSE = 1
+
+
+class _Pass(ctypes.Structure):
+    _fields_ = [
+        ("eye", ctypes.c_float * 3),
+        ("ambient", ctypes.c_float * 3),
+        ("fresnel_r0", ctypes.c_float * 3),
+        ("opacity", ctypes.c_float),
+        ("n_dir", ctypes.c_int32),
+        ("n_point", ctypes.c_int32),
+        ("n_spot", ctypes.c_int32),
+        ("ambient_mode", ctypes.c_int32),
+        ("use_f0_plane", ctypes.c_int32),
+        ("apply_ao", ctypes.c_int32),
+    ]
+
+
+@dataclass
+class OraclePass:
+    """Per-frame constants, mirroring cbPass/cbMaterial (Core.hlsl:35-81)."""
+    eye: tuple = (0.0, 0.0, -5.0)
+    ambient: tuple = (0.03, 0.03, 0.03)
+    fresnel_r0: tuple = (0.04, 0.04, 0.04)
+    opacity: float = 1.0
+    n_dir: int = 0
+    n_point: int = 0
+    n_spot: int = 0
+    ambient_mode: int = AMBIENT_CONSTANT
+    use_f0_plane: bool = False
+    apply_ao: bool = False
+
+    def to_c(self) -> _Pass:
+        p = _Pass()
+        p.eye[:] = [float(v) for v in self.eye]
+        p.ambient[:] = [float(v) for v in self.ambient]
+        p.fresnel_r0[:] = [float(v) for v in self.fresnel_r0]
+        p.opacity = float(self.opacity)
+        p.n_dir, p.n_point, p.n_spot = int(self.n_dir), int(self.n_point), int(self.n_spot)
+        p.ambient_mode = int(self.ambient_mode)
+        p.use_f0_plane = int(bool(self.use_f0_plane))
+        p.apply_ao = int(bool(self.apply_ao))
+        return p
+
+
+_libs: dict = {}
+
+
+def build(ref: bool = False) -> None:
+    """Compile liboracle.so (and, when /root/reference exists and ref=True, _ref/libpbr_ref.so)."""
+    targets = ["liboracle.so"]
+    if ref and os.path.exists(REFERENCE_SHADER):
+        targets.append("ref")
+    subprocess.run(["make", "-s", "-C", HERE] + targets, check=True)
+
+
+def _load(path: str, sym: str):
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C {HERE}`")
+        lib = ctypes.CDLL(path)
+        fn = getattr(lib, sym)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),
+                       ctypes.POINTER(_Pass), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
+        _libs[path] = fn
+    return _libs[path]
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_SO)
+
+
+def _shade(fn, planes, opass: OraclePass, lights, env, n_threads: int) -> np.ndarray:
+    """planes: sequence of NUM_PLANES arrays (or None), each (H, W) float32 C-contiguous."""
+    assert len(planes) == NUM_PLANES
+    ref_plane = next(p for p in planes if p is not None)
+    h, w = ref_plane.shape
+    keep = []
+    ptrs = (ctypes.c_void_p * NUM_PLANES)()
+    for i, p in enumerate(planes):
+        if p is None:
+            ptrs[i] = None
+            continue
+        a = np.ascontiguousarray(p, dtype=np.float32)
+        assert a.shape == (h, w)
+        keep.append(a)
+        ptrs[i] = a.ctypes.data
+    n_lights = opass.n_dir + opass.n_point + opass.n_spot
+    lights_arr = np.ascontiguousarray(lights, dtype=np.float32).reshape(-1, 12) if n_lights else np.zeros((1, 12), np.float32)
+    assert lights_arr.shape[0] >= n_lights
+    env_ptr, ew, eh = None, 0, 0
+    if env is not None:
+        env_arr = np.ascontiguousarray(env, dtype=np.uint16)
+        assert env_arr.ndim == 3 and env_arr.shape[2] == 4
+        eh, ew = env_arr.shape[:2]
+        keep.append(env_arr)
+        env_ptr = env_arr.ctypes.data
+    out = np.empty((h, w, 4), np.float32)
+    cp = opass.to_c()
+    rc = fn(w, h, w, ptrs, ctypes.byref(cp), lights_arr.ctypes.data, env_ptr, ew, eh,
+            out.ctypes.data, w, int(n_threads))
+    if rc != 0:
+        raise ValueError(f"oracle rejected arguments (rc={rc})")
+    return out
+
+
+def shade(planes, opass: OraclePass, lights=None, env=None, n_threads: int = 1) -> np.ndarray:
+    """The C restatement (pbr_oracle.c)."""
+    return _shade(_load(ORACLE_SO, "oracle_shade"), planes, opass, lights, env, n_threads)
+
+
+def shade_ref(planes, opass: OraclePass, lights=None, env=None) -> np.ndarray:
+    """The reference's LightingUtil.hlsl compiled as C++ (oracle/_ref); this container only."""
+    return _shade(_load(REF_SO, "ref_shade"), planes, opass, lights, env, 1)
+
+
+def rel_err(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Per-channel relative error |a-b| / max(|b|, 1e-30); NaN==NaN counts as 0, NaN vs number as inf."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        e = np.abs(a.astype(np.float64) - b.astype(np.float64)) / np.maximum(np.abs(b.astype(np.float64)), 1e-30)
+    e = np.where(na & nb, 0.0, e)
+    e = np.where(na ^ nb, np.inf, e)
+    same_inf = np.isinf(a) & np.isinf(b) & (a == b)
+    return np.where(same_inf, 0.0, e)
+
+
+def bit_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Elementwise bit equality, treating any NaN as equal to any NaN."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    return (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))

@@ -1,0 +1,168 @@
+"""ctypes binding of ``include/pbr/pbr_shade.h`` (libpbrshade.so, built in-tree for gfx950).
+
+There is no fallback: if the HIP library is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "_lib", "libpbrshade.so")
+HEADER_PATH = os.path.join(REPO_DIR, "include", "pbr", "pbr_shade.h")
+CSRC_DIR = os.path.join(PKG_DIR, "csrc")
+
+PBR_OK = 0
+PBR_MAX_LIGHTS = 4096
+PBR_AMBIENT_CONSTANT = 0
+PBR_AMBIENT_IBL_DIFFUSE = 1
+PBR_FLAG_F0_PLANE = 1 << 0
+PBR_FLAG_APPLY_AO = 1 << 1
+PBR_FLAG_TILED_CULLING = 1 << 2
+PBR_SCENE_SPHERE_RUSTEDIRON = 1
+PBR_SCENE_RANDOM_COVERED = 2
+PBR_SCENE_PLANE_MATERIALS = 4
+
+NUM_PLANES = 15
+PLANE_NAMES = ("px", "py", "pz", "nx", "ny", "nz", "ar", "ag", "ab",
+               "metal", "rough", "ao", "f0r", "f0g", "f0b")
+
+
+class PbrError(RuntimeError):
+    def __init__(self, status: int, what: str, detail: str = ""):
+        self.status = status
+        msg = f"{what} failed: {status_string(status)} ({status})"
+        if detail:
+            msg += f": {detail}"
+        super().__init__(msg)
+
+
+class Light(ctypes.Structure):
+    """The reference cbuffer `Light` (LightingUtil.hlsl:9-17), 48 bytes."""
+    _fields_ = [
+        ("strength", ctypes.c_float * 3),
+        ("spot_power", ctypes.c_float),
+        ("direction", ctypes.c_float * 3),
+        ("pad0", ctypes.c_float),
+        ("position", ctypes.c_float * 3),
+        ("pad1", ctypes.c_float),
+    ]
+
+
+class PassDesc(ctypes.Structure):
+    _fields_ = [
+        ("eye_pos_w", ctypes.c_float * 3),
+        ("ambient_light", ctypes.c_float * 3),
+        ("fresnel_r0", ctypes.c_float * 3),
+        ("opacity", ctypes.c_float),
+        ("num_dir_lights", ctypes.c_int32),
+        ("num_point_lights", ctypes.c_int32),
+        ("num_spot_lights", ctypes.c_int32),
+        ("ambient_mode", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("lights", ctypes.POINTER(Light)),
+    ]
+
+
+class GBufferSoA(ctypes.Structure):
+    _fields_ = [
+        ("pos_w", ctypes.c_void_p * 3),
+        ("normal_w", ctypes.c_void_p * 3),
+        ("albedo", ctypes.c_void_p * 3),
+        ("metallic", ctypes.c_void_p),
+        ("roughness", ctypes.c_void_p),
+        ("ao", ctypes.c_void_p),
+        ("f0", ctypes.c_void_p * 3),
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("row_stride", ctypes.c_int64),
+    ]
+
+
+class SceneAssets(ctypes.Structure):
+    _fields_ = [
+        ("rust_metallic", ctypes.c_void_p),
+        ("rust_roughness", ctypes.c_void_p),
+        ("rust_size", ctypes.c_int32),
+        ("mat_albedo", ctypes.c_void_p),
+        ("mat_specular", ctypes.c_void_p),
+        ("mat_roughness", ctypes.c_void_p),
+        ("mat_metallic", ctypes.c_void_p),
+        ("mat_has_metallic", ctypes.c_void_p),
+        ("mat_normal", ctypes.c_void_p),
+        ("num_materials", ctypes.c_int32),
+        ("mat_size", ctypes.c_int32),
+    ]
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("assets", ctypes.POINTER(SceneAssets)),
+    ]
+
+
+# name -> (restype, argtypes); every symbol declared in the header must appear here.
+SIGNATURES = {
+    "pbr_context_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "pbr_context_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "pbr_set_pass": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(PassDesc), ctypes.c_void_p]),
+    "pbr_set_env_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_void_p]),
+    "pbr_shade_gbuffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GBufferSoA), ctypes.c_void_p,
+                                         ctypes.c_int64, ctypes.c_void_p]),
+    "pbr_last_cull_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                           ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "pbr_gbuffer_fill": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int32]),
+    "pbr_scene_pass": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.POINTER(Light),
+                                      ctypes.POINTER(PassDesc)]),
+    "pbr_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "pbr_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "pbr_abi_version": (ctypes.c_int, []),
+}
+
+_lib = None
+
+
+def header_symbols(path: str = HEADER_PATH) -> list:
+    """Function names declared in the public header (for the ABI-coverage test)."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pbr_[a-z_0-9]+)\s*\(", text)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libpbrshade.so. Raises (never falls back) if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C {CSRC_DIR}` or __graft_entry__.build()")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def status_string(status: int) -> str:
+    try:
+        return lib().pbr_strerror(int(status)).decode()
+    except Exception:  # pragma: no cover - the message path must never mask the original error
+        return "unknown"
+
+
+def check(status: int, what: str, ctx=None) -> int:
+    if status < 0:
+        detail = ""
+        if ctx:
+            detail = (lib().pbr_last_error(ctx) or b"").decode()
+        raise PbrError(int(status), what, detail)
+    return status

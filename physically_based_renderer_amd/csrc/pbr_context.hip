@@ -1,0 +1,292 @@
+// pbr_context.hip -- the C ABI of include/pbr/pbr_shade.h: context lifetime, pass/env upload and
+// the shade entry point. Host code only; the kernels live in shade_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "pbr/pbr_shade.h"
+#include "shade_kernels.h"
+
+struct pbr_context {
+    int device = 0;
+    // Lights: device copy (3 float4 per light) fed from a small pinned ring so a host pass struct can
+    // be reused as soon as pbr_set_pass returns while the copy is still in flight.
+    float4* d_lights = nullptr;
+    int lights_capacity = 0;
+    static constexpr int kRing = 4;
+    pbr_light* h_ring[kRing] = {};
+    hipEvent_t ring_done[kRing] = {};
+    bool ring_used[kRing] = {};
+    int ring_next = 0;
+    // Environment: u16 upload buffer and the decoded fp32 RGBA texture.
+    uint16_t* d_env_u16 = nullptr;
+    float4* d_env = nullptr;
+    int env_w = 0, env_h = 0, env_capacity = 0;
+    // Current pass.
+    pbr::PassArgs pass{};
+    int ambient_mode = 0;
+    uint32_t flags = 0;
+    bool pass_set = false;
+    unsigned long long* d_cull_stats = nullptr;
+    std::string last_error;
+    std::mutex mu;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int fail_hip(pbr_context* ctx, hipError_t e, const char* what, int status = PBR_ERR_HIP) {
+    if (ctx) {
+        ctx->last_error = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+    }
+    return e == hipErrorOutOfMemory ? PBR_ERR_OUT_OF_MEMORY : status;
+}
+
+bool is_ambient_mode(int m) { return m == PBR_AMBIENT_CONSTANT || m == PBR_AMBIENT_IBL_DIFFUSE; }
+
+}  // namespace
+
+extern "C" {
+
+int pbr_abi_version(void) { return PBR_ABI_VERSION; }
+
+const char* pbr_strerror(int status) {
+    switch (status) {
+        case PBR_OK: return "ok";
+        case PBR_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case PBR_ERR_NO_DEVICE: return "no HIP device";
+        case PBR_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case PBR_ERR_LAUNCH: return "kernel launch failed";
+        case PBR_ERR_HIP: return "HIP runtime error";
+        case PBR_ERR_NOT_READY: return "pass or environment map not set";
+        case PBR_ERR_UNSUPPORTED: return "unsupported";
+        default: return "unknown status";
+    }
+}
+
+const char* pbr_last_error(const pbr_context* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+int pbr_context_create(int device, pbr_context** out_ctx) {
+    if (!out_ctx) return PBR_ERR_INVALID_ARGUMENT;
+    *out_ctx = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return PBR_ERR_NO_DEVICE;
+    if (device < 0 || device >= count) return PBR_ERR_INVALID_ARGUMENT;
+    pbr_context* ctx = new (std::nothrow) pbr_context();
+    if (!ctx) return PBR_ERR_OUT_OF_MEMORY;
+    ctx->device = device;
+    DeviceGuard g(device);
+    if (!g.ok) {
+        delete ctx;
+        return PBR_ERR_NO_DEVICE;
+    }
+    hipError_t e = hipMalloc(&ctx->d_cull_stats, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(ctx->d_cull_stats, 0, 2 * sizeof(unsigned long long));
+    for (int i = 0; e == hipSuccess && i < pbr_context::kRing; ++i) {
+        e = hipHostMalloc(reinterpret_cast<void**>(&ctx->h_ring[i]), sizeof(pbr_light) * PBR_MAX_LIGHTS,
+                          hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ring_done[i], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        pbr_context_destroy(ctx);
+        return e == hipErrorOutOfMemory ? PBR_ERR_OUT_OF_MEMORY : PBR_ERR_HIP;
+    }
+    *out_ctx = ctx;
+    return PBR_OK;
+}
+
+int pbr_context_destroy(pbr_context* ctx) {
+    if (!ctx) return PBR_ERR_INVALID_ARGUMENT;
+    {
+        DeviceGuard g(ctx->device);
+        (void)hipDeviceSynchronize();
+        for (int i = 0; i < pbr_context::kRing; ++i) {
+            if (ctx->ring_done[i]) (void)hipEventDestroy(ctx->ring_done[i]);
+            if (ctx->h_ring[i]) (void)hipHostFree(ctx->h_ring[i]);
+        }
+        if (ctx->d_lights) (void)hipFree(ctx->d_lights);
+        if (ctx->d_env_u16) (void)hipFree(ctx->d_env_u16);
+        if (ctx->d_env) (void)hipFree(ctx->d_env);
+        if (ctx->d_cull_stats) (void)hipFree(ctx->d_cull_stats);
+    }
+    delete ctx;
+    return PBR_OK;
+}
+
+int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
+    if (!ctx || !pass) return PBR_ERR_INVALID_ARGUMENT;
+    const int nd = pass->num_dir_lights, np = pass->num_point_lights, ns = pass->num_spot_lights;
+    if (nd < 0 || np < 0 || ns < 0) return PBR_ERR_INVALID_ARGUMENT;
+    const long long n = (long long)nd + np + ns;
+    if (n > PBR_MAX_LIGHTS) return PBR_ERR_INVALID_ARGUMENT;
+    if (n > 0 && !pass->lights) return PBR_ERR_INVALID_ARGUMENT;
+    if (!is_ambient_mode(pass->ambient_mode)) return PBR_ERR_INVALID_ARGUMENT;
+    const uint32_t known = PBR_FLAG_F0_PLANE | PBR_FLAG_APPLY_AO | PBR_FLAG_TILED_CULLING;
+    if (pass->flags & ~known) return PBR_ERR_INVALID_ARGUMENT;
+
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return PBR_ERR_NO_DEVICE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (n > ctx->lights_capacity) {
+        // Growing: the old buffer may still be read by queued kernels on any stream.
+        if (ctx->d_lights) {
+            e = hipDeviceSynchronize();
+            if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass sync");
+            (void)hipFree(ctx->d_lights);
+            ctx->d_lights = nullptr;
+            ctx->lights_capacity = 0;
+        }
+        int cap = 64;
+        while (cap < n) cap *= 2;
+        e = hipMalloc(&ctx->d_lights, sizeof(pbr_light) * (size_t)cap);
+        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass hipMalloc");
+        ctx->lights_capacity = cap;
+    }
+    if (n > 0) {
+        const int slot = ctx->ring_next;
+        ctx->ring_next = (slot + 1) % pbr_context::kRing;
+        if (ctx->ring_used[slot]) {
+            e = hipEventSynchronize(ctx->ring_done[slot]);
+            if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass ring wait");
+        }
+        std::memcpy(ctx->h_ring[slot], pass->lights, sizeof(pbr_light) * (size_t)n);
+        e = hipMemcpyAsync(ctx->d_lights, ctx->h_ring[slot], sizeof(pbr_light) * (size_t)n, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass copy");
+        e = hipEventRecord(ctx->ring_done[slot], s);
+        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass record");
+        ctx->ring_used[slot] = true;
+    }
+    pbr::PassArgs& p = ctx->pass;
+    for (int i = 0; i < 3; ++i) {
+        p.eye[i] = pass->eye_pos_w[i];
+        p.ambient[i] = pass->ambient_light[i];
+        p.fresnel_r0[i] = pass->fresnel_r0[i];
+    }
+    p.opacity = pass->opacity;
+    p.n_dir = nd;
+    p.n_point = np;
+    p.n_spot = ns;
+    ctx->ambient_mode = pass->ambient_mode;
+    ctx->flags = pass->flags;
+    ctx->pass_set = true;
+    return PBR_OK;
+}
+
+int pbr_set_env_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int32_t height, void* stream) {
+    if (!ctx || !texels || width <= 0 || height <= 0) return PBR_ERR_INVALID_ARGUMENT;
+    if ((long long)width * height > (1ll << 26)) return PBR_ERR_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return PBR_ERR_NO_DEVICE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int n = width * height;
+    hipError_t e;
+    if (n > ctx->env_capacity) {
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_env_map sync");
+        if (ctx->d_env_u16) (void)hipFree(ctx->d_env_u16);
+        if (ctx->d_env) (void)hipFree(ctx->d_env);
+        ctx->d_env_u16 = nullptr;
+        ctx->d_env = nullptr;
+        ctx->env_capacity = 0;
+        e = hipMalloc(&ctx->d_env_u16, sizeof(uint16_t) * 4 * (size_t)n);
+        if (e == hipSuccess) e = hipMalloc(&ctx->d_env, sizeof(float4) * (size_t)n);
+        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_env_map hipMalloc");
+        ctx->env_capacity = n;
+    }
+    e = hipMemcpyAsync(ctx->d_env_u16, texels, sizeof(uint16_t) * 4 * (size_t)n, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_env_map copy");
+    e = pbr::launch_decode_env(ctx->d_env_u16, ctx->d_env, n, s);
+    if (e != hipSuccess) return fail_hip(ctx, e, "decode_env_kernel", PBR_ERR_LAUNCH);
+    // The host texels may be released on return: wait for the (pageable) copy to finish.
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_env_map sync");
+    ctx->env_w = width;
+    ctx->env_h = height;
+    return PBR_OK;
+}
+
+int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rgba, int64_t out_row_stride,
+                      void* stream) {
+    if (!ctx || !gb || !out_rgba) return PBR_ERR_INVALID_ARGUMENT;
+    if (gb->width < 0 || gb->height < 0 || gb->row_stride < gb->width || out_row_stride < gb->width)
+        return PBR_ERR_INVALID_ARGUMENT;
+    if (!ctx->pass_set) return PBR_ERR_NOT_READY;
+    const bool f0_plane = (ctx->flags & PBR_FLAG_F0_PLANE) != 0;
+    const bool apply_ao = (ctx->flags & PBR_FLAG_APPLY_AO) != 0;
+    const bool cull = (ctx->flags & PBR_FLAG_TILED_CULLING) != 0;
+    for (int i = 0; i < 3; ++i)
+        if (!gb->pos_w[i] || !gb->normal_w[i] || !gb->albedo[i]) return PBR_ERR_INVALID_ARGUMENT;
+    if (!gb->metallic || !gb->roughness) return PBR_ERR_INVALID_ARGUMENT;
+    if (apply_ao && !gb->ao) return PBR_ERR_INVALID_ARGUMENT;
+    if (f0_plane && (!gb->f0[0] || !gb->f0[1] || !gb->f0[2])) return PBR_ERR_INVALID_ARGUMENT;
+    if (ctx->ambient_mode == PBR_AMBIENT_IBL_DIFFUSE && !ctx->d_env) return PBR_ERR_NOT_READY;
+    if (gb->width == 0 || gb->height == 0) return PBR_OK;
+
+    pbr::LaunchArgs a{};
+    const float* planes[15] = {gb->pos_w[0], gb->pos_w[1], gb->pos_w[2], gb->normal_w[0], gb->normal_w[1],
+                               gb->normal_w[2], gb->albedo[0], gb->albedo[1], gb->albedo[2], gb->metallic,
+                               gb->roughness, gb->ao, gb->f0[0], gb->f0[1], gb->f0[2]};
+    for (int i = 0; i < 15; ++i) a.gb.plane[i] = planes[i] ? planes[i] : planes[0];
+    a.gb.width = gb->width;
+    a.gb.height = gb->height;
+    a.gb.row_stride = gb->row_stride;
+    a.ps = ctx->pass;
+    a.ps.env_w = ctx->env_w;
+    a.ps.env_h = ctx->env_h;
+    a.lights = ctx->d_lights;
+    a.env = ctx->d_env;
+    a.out = reinterpret_cast<float4*>(out_rgba);
+    a.out_stride = out_row_stride;
+    a.cull_stats = ctx->d_cull_stats;
+    a.ambient_mode = ctx->ambient_mode;
+    a.f0_plane = f0_plane;
+    a.apply_ao = apply_ao;
+    a.cull = cull;
+    if ((reinterpret_cast<uintptr_t>(out_rgba) & 15u) != 0) return PBR_ERR_INVALID_ARGUMENT;  // float4 stores
+
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return PBR_ERR_NO_DEVICE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (cull) {
+        e = hipMemsetAsync(ctx->d_cull_stats, 0, 2 * sizeof(unsigned long long), s);
+        if (e != hipSuccess) return fail_hip(ctx, e, "cull stats reset");
+    }
+    e = pbr::launch_shade(a, s);
+    if (e != hipSuccess) return fail_hip(ctx, e, "shade_tile_kernel launch", PBR_ERR_LAUNCH);
+    return PBR_OK;
+}
+
+int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream) {
+    if (!ctx || !sum_tile_lights || !num_tiles) return PBR_ERR_INVALID_ARGUMENT;
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return PBR_ERR_NO_DEVICE;
+    unsigned long long h[2] = {0, 0};
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = hipMemcpyAsync(h, ctx->d_cull_stats, sizeof(h), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail_hip(ctx, e, "pbr_last_cull_stats");
+    *sum_tile_lights = (int64_t)h[0];
+    *num_tiles = (int64_t)h[1];
+    return PBR_OK;
+}
+
+}  // extern "C"

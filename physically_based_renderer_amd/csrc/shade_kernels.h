@@ -1,0 +1,45 @@
+// shade_kernels.h -- internal launch interface between the C-ABI layer and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace pbr {
+
+constexpr int kAmbientConstant = 0;
+constexpr int kAmbientIblDiffuse = 1;
+
+// The 15 SoA planes in pbr_gbuffer_soa order: pos xyz, normal xyz, albedo rgb, metallic,
+// roughness, ao, f0 rgb. Unused planes may alias plane 0 (they are never read).
+struct GBufferArgs {
+    const float* plane[15];
+    int width, height;
+    int64_t row_stride;
+};
+
+// Pass constants passed by value as kernel arguments (the shading subset of cbPass / cbMaterial).
+struct PassArgs {
+    float eye[3];
+    float ambient[3];
+    float fresnel_r0[3];
+    float opacity;
+    int n_dir, n_point, n_spot;
+    int env_w, env_h;
+};
+
+struct LaunchArgs {
+    GBufferArgs gb;
+    PassArgs ps;
+    const float4* lights;  // 3 float4 per light (the reference's 48-byte Light)
+    const float4* env;     // env_w * env_h RGBA fp32, or nullptr
+    float4* out;
+    int64_t out_stride;    // pixels
+    unsigned long long* cull_stats;  // [sum kept lights, tiles], CULL only
+    int ambient_mode;
+    bool f0_plane, apply_ao, cull;
+};
+
+hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);
+hipError_t launch_decode_env(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream);
+
+}  // namespace pbr

@@ -1,0 +1,112 @@
+"""Row-band partitioning of the framebuffer across GPUs and RCCL gather of the shaded bands.
+
+Pixels are independent in the reference's pixel shader (``Default.hlsl:47-161`` reads nothing but its
+own fragment and the constants), so a frame splits into horizontal bands with no data exchange while
+shading; the one real exchange is assembling the final image on rank 0 (BASELINE config 5:
+8192x8192 over 8 GPUs). One process per GPU, ``torch.distributed`` with the ``nccl`` backend
+(RCCL over xGMI on MI355X); ``gloo`` runs the same code on CPU tensors for tests.
+
+The G-buffer fill is a function of the global pixel only (``pbr_gbuffer_fill``), so every rank
+generates exactly its own rows and the gathered image is bit-identical to a single-GPU frame.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass(frozen=True)
+class Band:
+    rank: int
+    world: int
+    row_begin: int
+    row_end: int
+    rows_max: int  # rows of the largest band (gather slot height)
+
+    @property
+    def rows(self) -> int:
+        return self.row_end - self.row_begin
+
+
+def band_rows(height: int, world: int, rank: int, align: int = 8) -> Band:
+    """Rank ``rank``'s rows: equal bands rounded to ``align`` rows (the 8-row shading tile), the
+    remainder going to the last ranks so that every band but the tail is tile-aligned."""
+    if world < 1 or not 0 <= rank < world or height < 0:
+        raise ValueError("bad partition")
+    tiles = (height + align - 1) // align
+    per, extra = divmod(tiles, world)
+
+    def start(r: int) -> int:
+        return min(height, align * (r * per + max(0, r - (world - extra))))
+
+    r0, r1 = start(rank), start(rank + 1)
+    rows_max = min(height, align * (per + (1 if extra else 0)))
+    return Band(rank, world, r0, r1, rows_max)
+
+
+def all_bands(height: int, world: int, align: int = 8) -> List[Band]:
+    return [band_rows(height, world, r, align) for r in range(world)]
+
+
+def init_from_env(backend: str) -> Tuple[int, int, int]:
+    """(rank, world, local_rank) from torchrun's environment; initialises the default group once."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        kwargs = {}
+        if backend == "nccl":
+            kwargs["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
+    return rank, world, local
+
+
+class BandGather:
+    """Gathers every rank's (rows_max, W, 4) band into rank 0's (world, rows_max, W, 4) buffer.
+
+    Implemented as one grouped point-to-point round (each peer sends its band straight to rank 0
+    over its own xGMI link; rank 0 posts one receive per peer) rather than a ring all-gather: only
+    rank 0 needs the image, and a star puts all 7 links into rank 0 to work at once.
+    """
+
+    def __init__(self, band: Band, width: int, device, group=None, dtype=torch.float32):
+        self.band = band
+        self.group = group
+        self.width = width
+        self.frame: Optional[torch.Tensor] = None
+        if band.rank == 0:
+            self.frame = torch.empty((band.world, band.rows_max, width, 4), dtype=dtype, device=device)
+
+    def start(self, band_out: torch.Tensor):
+        """Post the gather of ``band_out`` ((rows_max, W, 4)); returns the list of work handles."""
+        b = self.band
+        if b.world == 1:
+            self.frame[0].copy_(band_out)
+            return []
+        if b.rank == 0:
+            self.frame[0].copy_(band_out)
+            ops = [dist.P2POp(dist.irecv, self.frame[r], r, self.group) for r in range(1, b.world)]
+        else:
+            ops = [dist.P2POp(dist.isend, band_out, 0, self.group)]
+        return dist.batch_isend_irecv(ops)
+
+    @staticmethod
+    def wait(handles) -> None:
+        for h in handles:
+            h.wait()
+
+    def assembled(self, height: int) -> Optional[torch.Tensor]:
+        """Rank 0: the (height, W, 4) image stitched from the gathered slots (a copy when bands are
+        uneven, else a view)."""
+        if self.frame is None:
+            return None
+        bands = all_bands(height, self.band.world)
+        if all(b.rows == self.band.rows_max for b in bands):
+            return self.frame.reshape(-1, self.width, 4)[:height]
+        return torch.cat([self.frame[b.rank, : b.rows] for b in bands], dim=0)

@@ -1,0 +1,219 @@
+"""Host-side mirror of the reference's shading interface, over the C ABI of libpbrshade.so.
+
+The reference drives its pixel shader through D3D12: per-frame constants in ``PassConstants``
+(``Source/App/FrameResource.h:19-44``) holding ``Light Lights[MaxLights]`` (``d3dUtil.h:144-152``),
+per-material constants (``Material.h:10-29``), then ``DrawIndexedInstanced`` (``PBRApp.cpp:1133``).
+Here the same roles are:
+
+  =====================================  ==============================================
+  reference                              this module
+  =====================================  ==============================================
+  ``Light`` (strength/spotpower/dir/pos)  :class:`Light` (same fields, same defaults)
+  ``PassConstants`` + light-count defines :class:`PassConstants`
+  ``UpdateMainPassCB`` / ``CopyData``     :meth:`ShadingContext.set_pass`
+  sky_env SRV (t1)                        :meth:`ShadingContext.set_env_map`
+  ``DrawIndexedInstanced(PS)``            :meth:`ShadingContext.shade`
+  =====================================  ==============================================
+
+PyTorch is used only for device memory and streams. Every shading call runs the gfx950 kernel;
+there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+
+@dataclass
+class Light:
+    """``struct Light`` (LightingUtil.hlsl:9-17) with the C++ defaults of d3dUtil.h:144-152."""
+    strength: Sequence[float] = (0.5, 0.5, 0.5)
+    spot_power: float = 64.0
+    direction: Sequence[float] = (0.0, -1.0, 0.0)
+    position: Sequence[float] = (0.0, 0.0, 0.0)
+
+    def to_c(self) -> N.Light:
+        c = N.Light()
+        c.strength[:] = [float(v) for v in self.strength]
+        c.spot_power = float(self.spot_power)
+        c.direction[:] = [float(v) for v in self.direction]
+        c.position[:] = [float(v) for v in self.position]
+        return c
+
+
+@dataclass
+class PassConstants:
+    """Shading subset of cbPass / cbMaterial (Core.hlsl:35-81) plus the NUM_*_LIGHTS defines.
+
+    ``lights`` are ordered directional, point, spot (ComputeLighting, LightingUtil.hlsl:176-199);
+    alternatively pass ``lights_array`` as an (n, 12) float32 array in the 48-byte layout.
+    """
+    eye_pos_w: Sequence[float] = (0.0, 0.0, -5.0)
+    ambient_light: Sequence[float] = (0.03, 0.03, 0.03)
+    fresnel_r0: Sequence[float] = (0.04, 0.04, 0.04)
+    opacity: float = 1.0
+    num_dir_lights: int = 0
+    num_point_lights: int = 0
+    num_spot_lights: int = 0
+    ambient_mode: int = N.PBR_AMBIENT_CONSTANT
+    flags: int = 0
+    lights: Sequence[Light] = field(default_factory=list)
+    lights_array: Optional[np.ndarray] = None
+
+    @property
+    def num_lights(self) -> int:
+        return self.num_dir_lights + self.num_point_lights + self.num_spot_lights
+
+    def light_array(self) -> np.ndarray:
+        if self.lights_array is not None:
+            arr = np.ascontiguousarray(self.lights_array, dtype=np.float32).reshape(-1, 12)
+        else:
+            arr = np.zeros((len(self.lights), 12), np.float32)
+            for i, L in enumerate(self.lights):
+                arr[i, 0:3] = L.strength
+                arr[i, 3] = L.spot_power
+                arr[i, 4:7] = L.direction
+                arr[i, 8:11] = L.position
+        if arr.shape[0] < self.num_lights:
+            raise ValueError(f"{self.num_lights} lights declared, {arr.shape[0]} given")
+        return arr
+
+    def to_c(self, keepalive: list) -> N.PassDesc:
+        p = N.PassDesc()
+        p.eye_pos_w[:] = [float(v) for v in self.eye_pos_w]
+        p.ambient_light[:] = [float(v) for v in self.ambient_light]
+        p.fresnel_r0[:] = [float(v) for v in self.fresnel_r0]
+        p.opacity = float(self.opacity)
+        p.num_dir_lights = int(self.num_dir_lights)
+        p.num_point_lights = int(self.num_point_lights)
+        p.num_spot_lights = int(self.num_spot_lights)
+        p.ambient_mode = int(self.ambient_mode)
+        p.flags = int(self.flags)
+        arr = self.light_array()
+        keepalive.append(arr)
+        p.lights = ctypes.cast(arr.ctypes.data, ctypes.POINTER(N.Light)) if arr.size else None
+        return p
+
+    @classmethod
+    def from_c(cls, p: N.PassDesc, lights: np.ndarray) -> "PassConstants":
+        return cls(eye_pos_w=tuple(p.eye_pos_w), ambient_light=tuple(p.ambient_light),
+                   fresnel_r0=tuple(p.fresnel_r0), opacity=p.opacity, num_dir_lights=p.num_dir_lights,
+                   num_point_lights=p.num_point_lights, num_spot_lights=p.num_spot_lights,
+                   ambient_mode=p.ambient_mode, flags=p.flags, lights_array=np.array(lights, np.float32))
+
+
+class GBuffer:
+    """Structure-of-arrays G-buffer: one (15, H, row_stride) fp32 tensor, plane order
+    pos xyz, normal xyz, albedo rgb, metallic, roughness, ao, f0 rgb (pbr_gbuffer_soa)."""
+
+    def __init__(self, planes: torch.Tensor, width: Optional[int] = None):
+        if planes.dim() != 3 or planes.shape[0] != N.NUM_PLANES or planes.dtype != torch.float32:
+            raise ValueError("planes must be a (15, H, W) float32 tensor")
+        if planes.stride(2) != 1 or planes.stride(0) % 1 != 0:
+            raise ValueError("planes rows must be contiguous")
+        self.planes = planes
+        self.height = planes.shape[1]
+        self.width = planes.shape[2] if width is None else width
+        self.row_stride = planes.stride(1)
+
+    @classmethod
+    def from_host(cls, planes: np.ndarray, device) -> "GBuffer":
+        t = torch.from_numpy(np.ascontiguousarray(planes, dtype=np.float32))
+        return cls(t.to(device))
+
+    def rows(self, r0: int, r1: int) -> "GBuffer":
+        """A row band (a view: shading it writes only those rows)."""
+        return GBuffer(self.planes[:, r0:r1, :], self.width)
+
+    def to_c(self) -> N.GBufferSoA:
+        g = N.GBufferSoA()
+        base = self.planes.data_ptr()
+        ps = self.planes.stride(0) * 4
+        ptr = [base + i * ps for i in range(N.NUM_PLANES)]
+        g.pos_w[:] = ptr[0:3]
+        g.normal_w[:] = ptr[3:6]
+        g.albedo[:] = ptr[6:9]
+        g.metallic, g.roughness, g.ao = ptr[9], ptr[10], ptr[11]
+        g.f0[:] = ptr[12:15]
+        g.width, g.height, g.row_stride = int(self.width), int(self.height), int(self.row_stride)
+        return g
+
+
+def _stream_handle(stream) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream)
+
+
+class ShadingContext:
+    """One ``pbr_context`` on one device."""
+
+    def __init__(self, device: int = 0):
+        self.lib = N.lib()
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        N.check(self.lib.pbr_context_create(self.device, ctypes.byref(h)), "pbr_context_create")
+        self._h = h
+        self.pass_constants: Optional[PassConstants] = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            self.lib.pbr_context_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_pass(self, pc: PassConstants, stream=None) -> None:
+        keep: list = []
+        p = pc.to_c(keep)
+        N.check(self.lib.pbr_set_pass(self._h, ctypes.byref(p), ctypes.c_void_p(_stream_handle(stream))),
+                "pbr_set_pass", self._h)
+        self.pass_constants = pc
+
+    def set_env_map(self, texels: np.ndarray, stream=None) -> None:
+        t = np.ascontiguousarray(texels, dtype=np.uint16)
+        if t.ndim != 3 or t.shape[2] != 4:
+            raise ValueError("env map must be (h, w, 4) uint16")
+        N.check(self.lib.pbr_set_env_map(self._h, t.ctypes.data, t.shape[1], t.shape[0],
+                                         ctypes.c_void_p(_stream_handle(stream))), "pbr_set_env_map", self._h)
+
+    def shade(self, gb: GBuffer, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Shade every pixel of ``gb`` into ``out`` ((H, >=W, 4) fp32 on the device), asynchronously."""
+        if out is None:
+            out = torch.empty((gb.height, gb.width, 4), dtype=torch.float32, device=gb.planes.device)
+        if out.dtype != torch.float32 or out.dim() != 3 or out.shape[2] != 4 or out.stride(2) != 1 or out.stride(1) != 4:
+            raise ValueError("out must be (H, W, 4) float32 with contiguous pixels")
+        if out.shape[0] < gb.height or out.shape[1] < gb.width:
+            raise ValueError("out is smaller than the G-buffer")
+        g = gb.to_c()
+        N.check(self.lib.pbr_shade_gbuffer(self._h, ctypes.byref(g), ctypes.c_void_p(out.data_ptr()),
+                                           out.stride(0) // 4, ctypes.c_void_p(_stream_handle(stream))),
+                "pbr_shade_gbuffer", self._h)
+        return out
+
+    def cull_stats(self, stream=None):
+        """(sum of surviving point/spot lights over tiles, tiles) of the last culled pass."""
+        s, t = ctypes.c_int64(), ctypes.c_int64()
+        N.check(self.lib.pbr_last_cull_stats(self._h, ctypes.byref(s), ctypes.byref(t),
+                                             ctypes.c_void_p(_stream_handle(stream))), "pbr_last_cull_stats", self._h)
+        return s.value, t.value

@@ -1,0 +1,185 @@
+"""GPU parity: the gfx950 kernel (through the C ABI) against the CPU oracle and the golden vectors.
+
+Tolerance (north_star): |gpu - cpu| <= 1e-5 * |cpu| per RGBA channel, fp32, NaN == NaN. The kernel
+uses the oracle's operation order, no FMA contraction and correctly rounded div/sqrt, so most
+channels are bit-identical; the residue comes from device powf/atan2f/asinf (ocml) vs glibc.
+Culled vs unculled and band vs full-frame comparisons are required to be bit-identical.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_names, load_golden, oracle_pass_from_constants, oracle_pass_from_meta
+from oracle import oracle as O
+from physically_based_renderer_amd import _native as N
+from physically_based_renderer_amd import scenes as S
+from physically_based_renderer_amd.renderer import GBuffer, PassConstants, ShadingContext
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-5
+
+
+def pass_from_meta(meta, lights):
+    flags = (N.PBR_FLAG_F0_PLANE if meta["use_f0_plane"] else 0) | (N.PBR_FLAG_APPLY_AO if meta["apply_ao"] else 0)
+    return PassConstants(eye_pos_w=meta["eye"], ambient_light=meta["ambient"], fresnel_r0=meta["fresnel_r0"],
+                         opacity=meta["opacity"], num_dir_lights=meta["n_dir"], num_point_lights=meta["n_point"],
+                         num_spot_lights=meta["n_spot"], ambient_mode=meta["ambient_mode"], flags=flags,
+                         lights_array=lights)
+
+
+def gpu_shade(ctx, planes, pc, env, device):
+    ctx.set_pass(pc)
+    if env is not None:
+        ctx.set_env_map(env)
+    gb = GBuffer.from_host(planes, device)
+    out = ctx.shade(gb)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def report(name, got, ref):
+    e = O.rel_err(got, ref)
+    exact = O.bit_equal(got, ref).mean()
+    print(f"{name}: max_rel={e.max():.3g} bit_exact={exact:.6f} n={ref.size}")
+    return e
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_vectors_on_gpu(name, shading_ctx, gpu, env_map):
+    planes, lights, meta, expected = load_golden(name)
+    pc = pass_from_meta(meta, lights)
+    got = gpu_shade(shading_ctx, planes, pc, env_map if meta["env"] else None, gpu)
+    e = report(name, got, expected)
+    assert e.max() <= REL_TOL
+    assert np.array_equal(np.isnan(got), np.isnan(expected))
+
+
+def config_parity(ctx, device, cfg, row_step=1, n_threads=16, env=None):
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    env = S.env_map() if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
+    got = gpu_shade(ctx, planes, pc, env, device)[::row_step]
+    ref = O.shade(list(np.ascontiguousarray(planes[:, ::row_step])), oracle_pass_from_constants(pc),
+                  pc.light_array(), env, n_threads=n_threads)
+    return got, ref, pc
+
+
+@pytest.mark.parametrize("cid,size,row_step", [(1, None, 1), (2, (640, 96), 1), (3, (512, 64), 1),
+                                               (4, (1024, 256), 1), (2, None, 1), (3, None, 16), (4, None, 16),
+                                               (5, (8192, 64), 1)])
+def test_config_parity(cid, size, row_step, shading_ctx, gpu):
+    cfg = S.CONFIGS[cid] if size is None else S.CONFIGS[cid].with_size(*size)
+    got, ref, _ = config_parity(shading_ctx, gpu, cfg, row_step)
+    e = report(f"{cfg.name} {cfg.width}x{cfg.height} step{row_step}", got, ref)
+    assert e.max() <= REL_TOL
+
+
+def test_tiled_culling_is_bit_exact(shading_ctx, gpu):
+    cfg = S.CONFIGS[4]
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    assert pc.flags & N.PBR_FLAG_TILED_CULLING
+    gb = GBuffer.from_host(planes, gpu)
+    shading_ctx.set_pass(pc)
+    culled = shading_ctx.shade(gb).clone()
+    kept, tiles = shading_ctx.cull_stats()
+    pc_full = PassConstants(**{**pc.__dict__, "flags": pc.flags & ~N.PBR_FLAG_TILED_CULLING})
+    shading_ctx.set_pass(pc_full)
+    full = shading_ctx.shade(gb)
+    torch.cuda.synchronize()
+    assert O.bit_equal(culled.cpu().numpy(), full.cpu().numpy()).all()
+    assert tiles == ((cfg.width + 31) // 32) * ((cfg.height + 7) // 8)
+    mean_kept = kept / tiles
+    print(f"cfg4 tiled culling: {mean_kept:.2f} of {cfg.n_lights} lights per 32x8 tile")
+    assert 0 < mean_kept < cfg.n_lights / 4
+
+
+def test_culling_with_nonfinite_positions(shading_ctx, gpu):
+    cfg = S.CONFIGS[4].with_size(256, 64)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    planes[0, 3, 5] = np.nan
+    planes[2, 40, 200] = np.inf
+    pc = S.scene_pass(cfg)
+    got = gpu_shade(shading_ctx, planes, pc, None, gpu)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=8)
+    assert report("cfg4 nonfinite", got, ref).max() <= REL_TOL
+
+
+def test_f0_plane_equals_metallic_workflow(shading_ctx, gpu):
+    cfg = S.CONFIGS[2].with_size(512, 64)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    a = gpu_shade(shading_ctx, planes, pc, None, gpu)
+    pc_f0 = PassConstants(**{**pc.__dict__, "flags": pc.flags | N.PBR_FLAG_F0_PLANE})
+    b = gpu_shade(shading_ctx, planes, pc_f0, None, gpu)
+    assert O.bit_equal(a, b).all()
+
+
+def test_row_band_equals_full_frame(shading_ctx, gpu):
+    cfg = S.CONFIGS[3].with_size(640, 200)
+    pc = S.scene_pass(cfg)
+    shading_ctx.set_pass(pc)
+    shading_ctx.set_env_map(S.env_map())
+    full = shading_ctx.shade(S.build_gbuffer(cfg, gpu)).cpu().numpy()
+    r0, r1 = 37, 151  # not tile aligned
+    band = shading_ctx.shade(S.build_gbuffer(cfg, gpu, r0, r1)).cpu().numpy()
+    assert O.bit_equal(band, full[r0:r1]).all()
+
+
+def test_many_lights_cross_chunks(shading_ctx, gpu, env_map):
+    rng = np.random.default_rng(5)
+    h, w = 40, 100  # partial tiles on both axes
+    p = np.zeros((15, h, w), np.float32)
+    p[0:3] = rng.uniform(-30, 30, (3, h, w))
+    n = rng.normal(size=(3, h, w))
+    p[3:6] = n / np.linalg.norm(n, axis=0)
+    p[6:15] = rng.uniform(0, 1, (9, h, w))
+    nd, npt, ns = 300, 700, 300
+    L = np.zeros((nd + npt + ns, 12), np.float32)
+    L[:, 0:3] = rng.uniform(0, 30, (len(L), 3))
+    L[:, 3] = rng.uniform(1, 64, len(L))
+    d = rng.normal(size=(len(L), 3))
+    L[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    L[:, 8:11] = rng.uniform(-150, 150, (len(L), 3))
+    for flags in (0, N.PBR_FLAG_TILED_CULLING | N.PBR_FLAG_APPLY_AO):
+        pc = PassConstants(num_dir_lights=nd, num_point_lights=npt, num_spot_lights=ns,
+                           ambient_mode=N.PBR_AMBIENT_IBL_DIFFUSE, flags=flags, lights_array=L)
+        got = gpu_shade(shading_ctx, p, pc, env_map, gpu)
+        ref = O.shade(list(p), oracle_pass_from_constants(pc), L, env_map, n_threads=8)
+        assert report(f"1300 lights flags={flags}", got, ref).max() <= REL_TOL
+
+
+def test_strided_output_and_empty(shading_ctx, gpu):
+    cfg = S.CONFIGS[2].with_size(96, 24)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    shading_ctx.set_pass(pc)
+    gb = GBuffer.from_host(planes, gpu)
+    big = torch.full((24, 128, 4), -1.0, device=gpu)
+    shading_ctx.shade(gb, big)
+    ref = gpu_shade(shading_ctx, planes, pc, None, gpu)
+    b = big.cpu().numpy()
+    assert O.bit_equal(b[:, :96], ref).all()
+    assert (b[:, 96:] == -1.0).all()  # nothing written past the row
+    empty = GBuffer(torch.zeros((15, 0, 96), device=gpu))
+    shading_ctx.shade(empty, torch.empty((0, 96, 4), device=gpu))
+
+
+def test_error_paths(gpu):
+    ctx = ShadingContext(0)
+    gb = GBuffer(torch.zeros((15, 8, 8), device=gpu))
+    with pytest.raises(N.PbrError) as ei:
+        ctx.shade(gb)
+    assert ei.value.status == -6  # PBR_ERR_NOT_READY: no pass yet
+    ctx.set_pass(PassConstants(ambient_mode=N.PBR_AMBIENT_IBL_DIFFUSE))
+    with pytest.raises(N.PbrError) as ei:
+        ctx.shade(gb)
+    assert ei.value.status == -6  # IBL without an environment map
+    with pytest.raises(N.PbrError) as ei:
+        ctx.set_pass(PassConstants(flags=1 << 10))
+    assert ei.value.status == -1
+    with pytest.raises(N.PbrError):
+        ctx.set_pass(PassConstants(num_point_lights=N.PBR_MAX_LIGHTS + 1,
+                                   lights_array=np.zeros((N.PBR_MAX_LIGHTS + 1, 12), np.float32)))
+    ctx.close()
