@@ -61,8 +61,10 @@ enum pbr_pass_flags {
     PBR_FLAG_F0_PLANE = 1u << 0,    /* F0 from the G-buffer (SPECULAR_TEXTURE permutation, Default.hlsl:91-92);
                                        otherwise F0 = lerp(fresnel_r0, albedo, metallic) (Default.hlsl:94-95) */
     PBR_FLAG_APPLY_AO = 1u << 1,    /* extension: ambient *= AO. The reference never reads its AO slot. */
-    PBR_FLAG_TILED_CULLING = 1u << 2 /* per-tile range culling of point/spot lights; output is
-                                        bit-identical to the unculled pass ("exact culling") */
+    PBR_FLAG_TILED_CULLING = 1u << 2, /* per-tile range culling of point/spot lights; output is
+                                         bit-identical to the unculled pass ("exact culling") */
+    PBR_FLAG_EXACT_ONLY = 1u << 3     /* validation mode: never take the exact fast division/sqrt path
+                                         ("exact fast path"); output is bit-identical, slower */
 };
 
 /* Per-frame constants: the shading subset of cbPass (Core.hlsl:35-61, FrameResource.h:19-44) and

@@ -21,6 +21,7 @@ PBR_AMBIENT_IBL_DIFFUSE = 1
 PBR_FLAG_F0_PLANE = 1 << 0
 PBR_FLAG_APPLY_AO = 1 << 1
 PBR_FLAG_TILED_CULLING = 1 << 2
+PBR_FLAG_EXACT_ONLY = 1 << 3
 PBR_SCENE_SPHERE_RUSTEDIRON = 1
 PBR_SCENE_RANDOM_COVERED = 2
 PBR_SCENE_PLANE_MATERIALS = 4

@@ -136,7 +136,7 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
     if (n > PBR_MAX_LIGHTS) return PBR_ERR_INVALID_ARGUMENT;
     if (n > 0 && !pass->lights) return PBR_ERR_INVALID_ARGUMENT;
     if (!is_ambient_mode(pass->ambient_mode)) return PBR_ERR_INVALID_ARGUMENT;
-    const uint32_t known = PBR_FLAG_F0_PLANE | PBR_FLAG_APPLY_AO | PBR_FLAG_TILED_CULLING;
+    const uint32_t known = PBR_FLAG_F0_PLANE | PBR_FLAG_APPLY_AO | PBR_FLAG_TILED_CULLING | PBR_FLAG_EXACT_ONLY;
     if (pass->flags & ~known) return PBR_ERR_INVALID_ARGUMENT;
 
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -225,10 +225,12 @@ int pbr_set_env_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int
 
 int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rgba, int64_t out_row_stride,
                       void* stream) {
-    if (!ctx || !gb || !out_rgba) return PBR_ERR_INVALID_ARGUMENT;
+    if (!ctx || !gb) return PBR_ERR_INVALID_ARGUMENT;
     if (gb->width < 0 || gb->height < 0 || gb->row_stride < gb->width || out_row_stride < gb->width)
         return PBR_ERR_INVALID_ARGUMENT;
     if (!ctx->pass_set) return PBR_ERR_NOT_READY;
+    if (gb->width == 0 || gb->height == 0) return PBR_OK;  // empty frame: nothing is read or written
+    if (!out_rgba) return PBR_ERR_INVALID_ARGUMENT;
     const bool f0_plane = (ctx->flags & PBR_FLAG_F0_PLANE) != 0;
     const bool apply_ao = (ctx->flags & PBR_FLAG_APPLY_AO) != 0;
     const bool cull = (ctx->flags & PBR_FLAG_TILED_CULLING) != 0;
@@ -238,7 +240,6 @@ int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rg
     if (apply_ao && !gb->ao) return PBR_ERR_INVALID_ARGUMENT;
     if (f0_plane && (!gb->f0[0] || !gb->f0[1] || !gb->f0[2])) return PBR_ERR_INVALID_ARGUMENT;
     if (ctx->ambient_mode == PBR_AMBIENT_IBL_DIFFUSE && !ctx->d_env) return PBR_ERR_NOT_READY;
-    if (gb->width == 0 || gb->height == 0) return PBR_OK;
 
     pbr::LaunchArgs a{};
     const float* planes[15] = {gb->pos_w[0], gb->pos_w[1], gb->pos_w[2], gb->normal_w[0], gb->normal_w[1],
@@ -260,6 +261,7 @@ int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rg
     a.f0_plane = f0_plane;
     a.apply_ao = apply_ao;
     a.cull = cull;
+    a.exact_only = (ctx->flags & PBR_FLAG_EXACT_ONLY) != 0;
     if ((reinterpret_cast<uintptr_t>(out_rgba) & 15u) != 0) return PBR_ERR_INVALID_ARGUMENT;  // float4 stores
 
     DeviceGuard g(ctx->device);

@@ -30,6 +30,63 @@ __device__ __forceinline__ f3 normalize3(f3 v) {
 }
 __device__ __forceinline__ float hlerp(float x, float y, float s) { return x + s * (y - x); }
 
+// ---- Exact fast paths --------------------------------------------------------------------------
+// With correctly rounded division/sqrt, hipcc expands x / y into
+//   v_div_scale(y), v_div_scale(x), r = v_rcp(y'), e = fma(-y', r, 1), r = fma(e, r, r),
+//   q = x' * r, t = fma(-y', q, x'), q = fma(t, r, q), t = fma(-y', q, x'), q = v_div_fmas(t, r, q),
+//   v_div_fixup(q, y, x)
+// and sqrt(x) into a scaled v_sqrt plus a +-1 ulp correction and a class fix-up. When the operands
+// lie in a window where the scale steps leave them unchanged and the fix-up has nothing to fix
+// (every operand and intermediate normal, no overflow), the sequences below are the SAME
+// operations on the same values, so they return bit-identical, correctly rounded results:
+//   div_nr:  0 < y in [2^-60, 2^60]; x == +-0, or |x| in [2^-96, 2^60] with |x / y| in
+//            [2^-120, 2^120] (so r, e, q and the residual t stay normal or exactly zero). The
+//            residual is formed as fma(y, q, -x) = -fma(-y, q, x), which for y > 0 also keeps the
+//            sign of a -0 numerator that the plain form loses before v_div_fixup restores it;
+//   sqrt_nr: x in [2^-96, 2^128), finite (no scaling, no class fix-up).
+// The light loop proves the window per pixel-light (PixelInvariants::fast_ok, the light's staged
+// flag and a few compares) and falls back to the compiler's full sequences otherwise; the
+// PBR_FLAG_EXACT_ONLY validation mode runs only the full sequences and must match bit for bit
+// (tests/test_gpu_parity.py::test_fast_path_is_bit_identical_to_exact_only).
+struct Recip {
+    float y, r;
+};
+__device__ __forceinline__ Recip recip_nr(float y) {
+    float r = __builtin_amdgcn_rcpf(y);
+    float e = __builtin_fmaf(-y, r, 1.0f);
+    return Recip{y, __builtin_fmaf(e, r, r)};
+}
+__device__ __forceinline__ float div_nr(float x, Recip d) {
+    float q = x * d.r;
+    float t = __builtin_fmaf(d.y, q, -x);
+    q = __builtin_fmaf(-t, d.r, q);
+    t = __builtin_fmaf(d.y, q, -x);
+    return __builtin_fmaf(-t, d.r, q);
+}
+__device__ __forceinline__ float sqrt_nr(float x) {
+    float s = __builtin_amdgcn_sqrtf(x);
+    float sm = __int_as_float(__float_as_int(s) - 1);
+    float sp = __int_as_float(__float_as_int(s) + 1);
+    float rm = __builtin_fmaf(-sm, s, x);
+    float rp = __builtin_fmaf(-sp, s, x);
+    s = (rm <= 0.0f) ? sm : s;
+    return (rp > 0.0f) ? sp : s;
+}
+// |x| in [lo, hi] (false for NaN); zero_or_in also accepts +-0.
+__device__ __forceinline__ bool in_win(float x, float lo, float hi) { return fabsf(x) >= lo && fabsf(x) <= hi; }
+__device__ __forceinline__ bool zero_or_in(float x, float lo, float hi) { return x == 0.0f || in_win(x, lo, hi); }
+
+// pow(x, 5.0) of FresnelSchlick (LightingUtil.hlsl:46) for x = 1 - saturate(.) in [0, 1]:
+// x^2 is exact in fp64 and x^5 carries at most 2^-52 relative error before the one rounding to
+// fp32, which made it correctly rounded on every float in [0, 1] we checked (glibc's powf is not:
+// 0.07% of its results are 1 ulp off). Five fp64/convert ops instead of ocml's ~40-op powf.
+__device__ __forceinline__ float pow5(float x) {
+    double d = (double)x;
+    double d2 = d * d;
+    double d4 = d2 * d2;
+    return (float)(d4 * d);
+}
+
 constexpr float kPi = 3.14159265359f;  // LightingUtil.hlsl:59, 103 (an fp32 literal in HLSL)
 constexpr float kInvGamma = 1.0f / 2.2f;  // Default.hlsl:155
 constexpr float kLightRange = 100.0f;     // LightingUtil.hlsl:131
@@ -44,7 +101,39 @@ struct PixelInvariants {
     float k, one_minus_k;   // GeometrySchlickGGX: k = (r+1)^2 / 8 on the unclamped roughness (:66-67)
     float ggx_v;            // GeometrySchlickGGX(NdotV) = ggx2 (:79)
     float four_n_dot_v;     // 4.0f * max(dot(N,V), 0) (:95, left operand of the product)
+    Recip r_pi;             // refined reciprocal of PI for the exact fast division by PI (:103)
+    bool fast_ok;           // the pixel's inputs lie in the fast-path window (see below)
 };
+
+// Per-pixel half of the fast-path proof ("exact fast path"). With every position
+// component (pixel and eye) zero or of magnitude [2^-20, 2^20], normal components zero or
+// [2^-20, 16], albedo/F0 components zero or [2^-20, 1024], metallic and roughness in [0, 1]:
+//   L = lightPos - P has components 0 or [2^-43, 2^21]; V and L/d components 0 or >= 2^-65;
+//   (V + L) components 0 or >= 2^-88; N.L is 0 or >= 2^-93; GeometrySchlickGGX's denominator is
+//   in [0.125, 48.5]; kD*albedo is 0 or in [2^-68, 2^21].
+// Together with the per-iteration compares in the light functions this keeps every fast-path
+// division and sqrt inside the windows stated above.
+__device__ __forceinline__ bool fast_window_ok(f3 pos, f3 eye, f3 n, f3 albedo, f3 f0, float metallic,
+                                               float roughness) {
+    const float lo = 0x1p-20f;
+    bool ok = zero_or_in(pos.x, lo, 0x1p20f) && zero_or_in(pos.y, lo, 0x1p20f) && zero_or_in(pos.z, lo, 0x1p20f);
+    ok = ok && zero_or_in(eye.x, lo, 0x1p20f) && zero_or_in(eye.y, lo, 0x1p20f) && zero_or_in(eye.z, lo, 0x1p20f);
+    ok = ok && zero_or_in(n.x, lo, 16.0f) && zero_or_in(n.y, lo, 16.0f) && zero_or_in(n.z, lo, 16.0f);
+    ok = ok && zero_or_in(albedo.x, lo, 1024.0f) && zero_or_in(albedo.y, lo, 1024.0f) &&
+         zero_or_in(albedo.z, lo, 1024.0f);
+    ok = ok && zero_or_in(f0.x, lo, 1024.0f) && zero_or_in(f0.y, lo, 1024.0f) && zero_or_in(f0.z, lo, 1024.0f);
+    ok = ok && metallic >= 0.0f && metallic <= 1.0f && roughness >= 0.0f && roughness <= 1.0f;
+    return ok;
+}
+
+// Per-light half, evaluated once when the light is staged: point/spot positions like pixel
+// positions; directional L = -Direction components zero or [2^-20, 16].
+__device__ __forceinline__ bool light_window_ok(bool directional, float4 dir, float4 pos) {
+    const float lo = 0x1p-20f;
+    if (directional)
+        return zero_or_in(dir.x, lo, 16.0f) && zero_or_in(dir.y, lo, 16.0f) && zero_or_in(dir.z, lo, 16.0f);
+    return zero_or_in(pos.x, lo, 0x1p20f) && zero_or_in(pos.y, lo, 0x1p20f) && zero_or_in(pos.z, lo, 0x1p20f);
+}
 
 __device__ __forceinline__ PixelInvariants make_invariants(f3 n, f3 v, f3 albedo, f3 f0, float metallic,
                                                            float roughness) {
@@ -65,63 +154,99 @@ __device__ __forceinline__ PixelInvariants make_invariants(f3 n, f3 v, f3 albedo
     float n_dot_v = hmax(dot3(n, v), 0.0f);
     q.ggx_v = n_dot_v / (n_dot_v * q.one_minus_k + q.k);
     q.four_n_dot_v = 4.0f * n_dot_v;
+    q.r_pi = recip_nr(kPi);
+    q.fast_ok = false;
     return q;
+}
+
+// x / d.y either through the exact fast sequence (FAST) or the compiler's full IEEE division.
+template <bool FAST>
+__device__ __forceinline__ float qdiv(float x, Recip d) {
+    return FAST ? div_nr(x, d) : x / d.y;
+}
+template <bool FAST>
+__device__ __forceinline__ Recip qrecip(float y) {
+    return FAST ? recip_nr(y) : Recip{y, 0.0f};
 }
 
 // BRDFCookTorrance (LightingUtil.hlsl:85-104) with DistributionGGX (:49-62), GeometrySmith (:75-83)
 // and FresnelSchlick (:43-47) inlined; returns (kD*albedo/PI + specular) * radiance * NdotL.
-__device__ __forceinline__ f3 brdf_cook_torrance(const PixelInvariants& q, f3 radiance, f3 l, f3 h) {
+// FAST: ANDs into `ok` the window conditions the pixel/light flags cannot guarantee.
+template <bool FAST>
+__device__ __forceinline__ f3 brdf_cook_torrance(const PixelInvariants& q, f3 radiance, f3 l, f3 h, bool& ok) {
     // DistributionGGX
     float n_dot_h = hmax(dot3(q.n, h), 0.0f);
     float n_dot_h_sqr = n_dot_h * n_dot_h;
     float den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
     den = kPi * den * den;
-    float ndf = q.a_sqr / den;
+    if (FAST) ok = ok && den >= 0x1p-60f && den <= 0x1p60f;
+    float ndf = qdiv<FAST>(q.a_sqr, qrecip<FAST>(den));
     // GeometrySmith: ggx1 * ggx2
     float n_dot_l = hmax(dot3(q.n, l), 0.0f);
-    float ggx_l = n_dot_l / (n_dot_l * q.one_minus_k + q.k);
+    float ggx_l = qdiv<FAST>(n_dot_l, qrecip<FAST>(n_dot_l * q.one_minus_k + q.k));
     float g = ggx_l * q.ggx_v;
     // FresnelSchlick(H, V, F0)
     float cos_theta = hsat(dot3(h, q.v));
-    float p = powf(1.0f - cos_theta, 5.0f);
+    float p = pow5(1.0f - cos_theta);
     f3 f = mk3(q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p);
-    // specular = (NDF*G)*F / (4*NdotV*NdotL + 0.001)
+    // specular = (NDF*G)*F / (4*NdotV*NdotL + 0.001); the denominator is >= 0.001 by construction
     float ndf_g = ndf * g;
     float denom = q.four_n_dot_v * n_dot_l + 0.001f;
-    f3 spec = mk3((ndf_g * f.x) / denom, (ndf_g * f.y) / denom, (ndf_g * f.z) / denom);
+    f3 nom = mk3(ndf_g * f.x, ndf_g * f.y, ndf_g * f.z);
+    if (FAST) {
+        ok = ok && zero_or_in(nom.x, 0x1p-60f, 0x1p60f) && zero_or_in(nom.y, 0x1p-60f, 0x1p60f) &&
+             zero_or_in(nom.z, 0x1p-60f, 0x1p60f) && denom <= 0x1p60f;
+    }
+    const Recip rdenom = qrecip<FAST>(denom);
+    f3 spec = mk3(qdiv<FAST>(nom.x, rdenom), qdiv<FAST>(nom.y, rdenom), qdiv<FAST>(nom.z, rdenom));
     // kD = (1 - F) * (1 - metallic)
     f3 kd = mk3((1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal);
-    return mk3((((kd.x * q.albedo.x) / kPi + spec.x) * radiance.x) * n_dot_l,
-               (((kd.y * q.albedo.y) / kPi + spec.y) * radiance.y) * n_dot_l,
-               (((kd.z * q.albedo.z) / kPi + spec.z) * radiance.z) * n_dot_l);
+    const Recip rpi = FAST ? q.r_pi : Recip{kPi, 0.0f};
+    return mk3(((qdiv<FAST>(kd.x * q.albedo.x, rpi) + spec.x) * radiance.x) * n_dot_l,
+               ((qdiv<FAST>(kd.y * q.albedo.y, rpi) + spec.y) * radiance.y) * n_dot_l,
+               ((qdiv<FAST>(kd.z * q.albedo.z, rpi) + spec.z) * radiance.z) * n_dot_l);
+}
+
+// normalize(v) through the fast path: sqrt_nr + three divisions sharing one refined reciprocal.
+template <bool FAST>
+__device__ __forceinline__ f3 normalize_q(f3 v, bool& ok) {
+    if (!FAST) return normalize3(v);
+    float s = sqrt_nr(dot3(v, v));
+    ok = ok && s >= 0x1p-30f && s <= 0x1p30f;
+    const Recip r = recip_nr(s);
+    return mk3(div_nr(v.x, r), div_nr(v.y, r), div_nr(v.z, r));
 }
 
 // ComputeDirectionalLight (LightingUtil.hlsl:109-119). The caller adds shadowFactor(1,1,1) * result,
 // and 1.0f * x == x exactly, so the multiply is omitted.
-__device__ __forceinline__ f3 directional_light(const PixelInvariants& q, float4 s, float4 d) {
+template <bool FAST>
+__device__ __forceinline__ f3 directional_light(const PixelInvariants& q, float4 s, float4 d, bool& ok) {
     f3 l = mk3(-d.x, -d.y, -d.z);
-    f3 h = normalize3(add3(q.v, l));
-    return brdf_cook_torrance(q, mk3(s.x, s.y, s.z), l, h);
+    f3 h = normalize_q<FAST>(add3(q.v, l), ok);
+    return brdf_cook_torrance<FAST>(q, mk3(s.x, s.y, s.z), l, h, ok);
 }
 
 // ComputePointLight (:124-142) / ComputeSpotLight (:147-167). Returns false when the range test at
 // :131 / :154 returns 0: adding +0 to the running sum is the identity (the sum starts at +0 and is
-// never -0), so skipping it is bit-exact.
-template <bool SPOT>
+// never -0), so skipping it is bit-exact. The range decision is exact on the fast path too: sqrt_nr
+// is exact on [2^-96, 2^128) and gives 0 / inf / NaN outside, all on the same side of 100.
+template <bool SPOT, bool FAST>
 __device__ __forceinline__ bool point_or_spot_light(const PixelInvariants& q, f3 pos, float4 s, float4 d, float4 p,
-                                                    f3& out) {
+                                                    f3& out, bool& ok) {
     f3 l = mk3(p.x - pos.x, p.y - pos.y, p.z - pos.z);
-    float dist = sqrtf(dot3(l, l));
+    float dist = FAST ? sqrt_nr(dot3(l, l)) : sqrtf(dot3(l, l));
     if (dist > kLightRange) return false;
-    l = mk3(l.x / dist, l.y / dist, l.z / dist);
-    f3 h = normalize3(add3(q.v, l));
-    float dsat = hmax(dist, 0.01f);  // CalcAttenuation (:35-40)
-    float att = 1.0f / (dsat * dsat);
+    if (FAST) ok = ok && dist >= 0x1p-20f;
+    const Recip rdist = qrecip<FAST>(dist);
+    l = mk3(qdiv<FAST>(l.x, rdist), qdiv<FAST>(l.y, rdist), qdiv<FAST>(l.z, rdist));
+    f3 h = normalize_q<FAST>(add3(q.v, l), ok);
+    float dsat = hmax(dist, 0.01f);  // CalcAttenuation (:35-40); dsat^2 in [1e-4, 1e4]
+    float att = qdiv<FAST>(1.0f, qrecip<FAST>(dsat * dsat));
     if (SPOT) {
         f3 nl = mk3(-l.x, -l.y, -l.z);
         att *= powf(hmax(dot3(nl, mk3(d.x, d.y, d.z)), 0.0f), s.w);  // :163, SpotPower in .w
     }
-    out = brdf_cook_torrance(q, mk3(s.x * att, s.y * att, s.z * att), l, h);
+    out = brdf_cook_torrance<FAST>(q, mk3(s.x * att, s.y * att, s.z * att), l, h, ok);
     return true;
 }
 

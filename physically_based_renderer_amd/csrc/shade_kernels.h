@@ -37,6 +37,7 @@ struct LaunchArgs {
     unsigned long long* cull_stats;  // [sum kept lights, tiles], CULL only
     int ambient_mode;
     bool f0_plane, apply_ao, cull;
+    bool exact_only;  // PBR_FLAG_EXACT_ONLY: skip the exact fast path (validation mode)
 };
 
 hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);

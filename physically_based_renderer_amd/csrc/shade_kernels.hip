@@ -49,9 +49,12 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // Stage lights [begin, begin+count) of the global list into LDS, culled against the tile when CULL.
 // Returns the number staged (identical in every work-item). Caller brackets with barriers.
+// Each staged record is the 48-byte Light with its unused pad1 (.w of the position float4)
+// replaced by the light's fast-path window flag (pbr_device_math.h, light_window_ok).
 template <bool CULL>
 __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, int begin, int count, float4* s_light,
-                                           int* s_wave_cnt, const TileBounds& tb, bool cull_enabled) {
+                                           int* s_wave_cnt, const TileBounds& tb, bool cull_enabled,
+                                           bool directional) {
     const int tid = threadIdx.x;
     const bool have = tid < count;
     float4 l0 = make_float4(0.f, 0.f, 0.f, 0.f), l1 = l0, l2 = l0;
@@ -60,6 +63,7 @@ __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, in
         l0 = src[0];
         l1 = src[1];
         l2 = src[2];
+        l2.w = light_window_ok(directional, l1, l2) ? 1.0f : 0.0f;
     }
     if (!CULL) {
         if (have) {
@@ -97,6 +101,27 @@ __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, in
     return total;
 }
 
+// One light's term of ComputeLighting: the exact fast path for every lane, then -- only if some lane
+// of the wave left the fast-path window -- the compiler's full IEEE sequences for those lanes. Both
+// produce the same bits wherever the fast path is taken, so the sum is independent of the choice.
+template <int KIND>  // 0 directional, 1 point, 2 spot
+__device__ __forceinline__ void accumulate_light(const PixelInvariants& q, f3 pos, const float4* rec, f3& direct) {
+    const float4 a = rec[0], b = rec[1], c = rec[2];
+    f3 col;
+    bool ok = q.fast_ok && c.w != 0.0f;
+    bool lit = true;
+    if (KIND == 0) col = directional_light<true>(q, a, b, ok);
+    else lit = point_or_spot_light<KIND == 2, true>(q, pos, a, b, c, col, ok);
+    if (__any(!ok)) {
+        if (!ok) {
+            bool unused = true;
+            if (KIND == 0) col = directional_light<false>(q, a, b, unused);
+            else lit = point_or_spot_light<KIND == 2, false>(q, pos, a, b, c, col, unused);
+        }
+    }
+    if (lit) direct = add3(direct, col);
+}
+
 }  // namespace
 
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
@@ -104,7 +129,8 @@ __global__ __launch_bounds__(kBlock) void shade_tile_kernel(GBufferArgs gb, Pass
                                                             const float4* __restrict__ lights,
                                                             const float4* __restrict__ env,
                                                             float4* __restrict__ out, int64_t out_stride,
-                                                            unsigned long long* __restrict__ cull_stats) {
+                                                            unsigned long long* __restrict__ cull_stats,
+                                                            bool exact_only) {
     __shared__ float4 s_light[3 * kChunk];
     __shared__ int s_wave_cnt[kBlock / 64];
     __shared__ float s_bounds[kBlock / 64][6];
@@ -130,7 +156,9 @@ __global__ __launch_bounds__(kBlock) void shade_tile_kernel(GBufferArgs gb, Pass
         f0 = mk3(hlerp(ps.fresnel_r0[0], albedo.x, metallic), hlerp(ps.fresnel_r0[1], albedo.y, metallic),
                  hlerp(ps.fresnel_r0[2], albedo.z, metallic));
     }
-    const PixelInvariants q = make_invariants(n, v, albedo, f0, metallic, roughness);
+    PixelInvariants q = make_invariants(n, v, albedo, f0, metallic, roughness);
+    q.fast_ok = !exact_only && fast_window_ok(pos, mk3(ps.eye[0], ps.eye[1], ps.eye[2]), n, albedo, f0, metallic,
+                                              roughness);
 
     TileBounds tb;
     bool cull_enabled = false;
@@ -165,38 +193,27 @@ __global__ __launch_bounds__(kBlock) void shade_tile_kernel(GBufferArgs gb, Pass
     for (int base = 0; base < ps.n_dir; base += kChunk) {
         const int cnt = min(kChunk, ps.n_dir - base);
         __syncthreads();
-        stage_chunk<false>(lights, base, cnt, s_light, s_wave_cnt, tb, false);
+        stage_chunk<false>(lights, base, cnt, s_light, s_wave_cnt, tb, false, true);
         __syncthreads();
-        for (int j = 0; j < cnt; ++j) {
-            const f3 c = directional_light(q, s_light[3 * j + 0], s_light[3 * j + 1]);
-            direct = add3(direct, c);
-        }
+        for (int j = 0; j < cnt; ++j) accumulate_light<0>(q, pos, &s_light[3 * j], direct);
     }
     // Point lights [n_dir, n_dir + n_point), then spot lights.
     const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
     for (int base = pt_begin; base < sp_begin; base += kChunk) {
         const int cnt = min(kChunk, sp_begin - base);
         __syncthreads();
-        const int kept = stage_chunk<CULL>(lights, base, cnt, s_light, s_wave_cnt, tb, cull_enabled);
+        const int kept = stage_chunk<CULL>(lights, base, cnt, s_light, s_wave_cnt, tb, cull_enabled, false);
         __syncthreads();
         kept_total += kept;
-        for (int j = 0; j < kept; ++j) {
-            f3 c;
-            if (point_or_spot_light<false>(q, pos, s_light[3 * j + 0], s_light[3 * j + 1], s_light[3 * j + 2], c))
-                direct = add3(direct, c);
-        }
+        for (int j = 0; j < kept; ++j) accumulate_light<1>(q, pos, &s_light[3 * j], direct);
     }
     for (int base = sp_begin; base < end; base += kChunk) {
         const int cnt = min(kChunk, end - base);
         __syncthreads();
-        const int kept = stage_chunk<CULL>(lights, base, cnt, s_light, s_wave_cnt, tb, cull_enabled);
+        const int kept = stage_chunk<CULL>(lights, base, cnt, s_light, s_wave_cnt, tb, cull_enabled, false);
         __syncthreads();
         kept_total += kept;
-        for (int j = 0; j < kept; ++j) {
-            f3 c;
-            if (point_or_spot_light<true>(q, pos, s_light[3 * j + 0], s_light[3 * j + 1], s_light[3 * j + 2], c))
-                direct = add3(direct, c);
-        }
+        for (int j = 0; j < kept; ++j) accumulate_light<2>(q, pos, &s_light[3 * j], direct);
     }
     if (CULL && tid == 0 && cull_stats != nullptr) {
         atomicAdd(&cull_stats[0], (unsigned long long)kept_total);
@@ -208,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void shade_tile_kernel(GBufferArgs gb, Pass
         // Default.hlsl:141-146: kS = FresnelSchlick(N, V, F0); kD = (1 - kS)(1 - metallic);
         // irradiance = env.Sample(linear-wrap, WorldToSkyUV(N)); ambient = kD * (irradiance * albedo)
         const float cos_theta = hsat(dot3(n, v));
-        const float p = powf(1.0f - cos_theta, 5.0f);
+        const float p = pow5(1.0f - cos_theta);
         const f3 ks = mk3(f0.x + q.one_minus_f0.x * p, f0.y + q.one_minus_f0.y * p, f0.z + q.one_minus_f0.z * p);
         const f3 kd = mk3((1.0f - ks.x) * q.one_minus_metal, (1.0f - ks.y) * q.one_minus_metal,
                           (1.0f - ks.z) * q.one_minus_metal);
@@ -246,7 +263,7 @@ template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
     dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
     hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream, a.gb,
-                       a.ps, a.lights, a.env, a.out, a.out_stride, a.cull_stats);
+                       a.ps, a.lights, a.env, a.out, a.out_stride, a.cull_stats, a.exact_only);
     return hipGetLastError();
 }
 

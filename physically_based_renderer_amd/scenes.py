@@ -106,8 +106,12 @@ def fill_gbuffer_host(cfg: SceneConfig, row_begin: int = 0, row_end: Optional[in
     assets = Assets.get()
     row_end = cfg.height if row_end is None else row_end
     rows = row_end - row_begin
+    if rows < 0 or row_begin < 0 or row_end > cfg.height:
+        raise N.PbrError(-1, "pbr_gbuffer_fill", f"rows [{row_begin}, {row_end}) outside [0, {cfg.height})")
     if out is None:
         out = np.empty((N.NUM_PLANES, rows, cfg.width), np.float32)
+    if rows == 0:
+        return out, 0
     assert out.dtype == np.float32 and out.shape[0] == N.NUM_PLANES and out.shape[1] >= rows
     assert out.strides[2] == 4 and out.strides[0] % 4 == 0
     ptrs = (ctypes.c_void_p * N.NUM_PLANES)(*[out[i].ctypes.data for i in range(N.NUM_PLANES)])

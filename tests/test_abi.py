@@ -1,0 +1,83 @@
+"""The C ABI (include/pbr/pbr_shade.h) of libpbrshade.so: it loads, exports every declared symbol,
+and validates arguments without touching a device."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT, gpu_available
+from physically_based_renderer_amd import _native as N
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = N.lib()
+    declared = N.header_symbols()
+    assert len(declared) >= 10
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in pbr_shade.h but not exported"
+        assert name in N.SIGNATURES, f"{name} has no ctypes signature"
+    assert set(N.SIGNATURES) == set(declared)
+    assert lib.pbr_abi_version() == 1
+
+
+def test_exports_are_c_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (pbr_\w+)$", out, flags=re.M))
+    assert set(N.header_symbols()) <= exported  # unmangled: extern "C"
+
+
+def test_library_is_built_for_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf" if os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf")
+                          else "readelf", "-S", N.LIB_PATH], capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in out
+    blob = open(N.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_struct_layouts_match_header():
+    assert ctypes.sizeof(N.Light) == 48  # LightingUtil.hlsl:9-17
+    assert N.Light.position.offset == 32
+    assert ctypes.sizeof(N.GBufferSoA) == 15 * 8 + 8 + 8
+    assert N.PassDesc.lights.offset == 64
+    assert ctypes.sizeof(N.SceneDesc) == 24 + 8
+
+
+def test_strerror_and_status_codes():
+    lib = N.lib()
+    assert lib.pbr_strerror(0) == b"ok"
+    for code in range(-7, 0):
+        assert lib.pbr_strerror(code) not in (b"", b"unknown status")
+    assert lib.pbr_strerror(-99) == b"unknown status"
+    assert lib.pbr_last_error(None) == b""
+
+
+def test_null_arguments_are_rejected_without_a_device():
+    lib = N.lib()
+    assert lib.pbr_context_create(0, None) == -1
+    assert lib.pbr_context_destroy(None) == -1
+    assert lib.pbr_set_pass(None, None, None) == -1
+    assert lib.pbr_set_env_map(None, None, 0, 0, None) == -1
+    assert lib.pbr_shade_gbuffer(None, None, None, 0, None) == -1
+    assert lib.pbr_last_cull_stats(None, None, None, None) == -1
+    assert lib.pbr_gbuffer_fill(None, 0, 0, None, 0, 1) == -1
+    assert lib.pbr_scene_pass(None, 0, None, None) == -1
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-device path")
+def test_context_create_without_device_reports_no_device():
+    h = ctypes.c_void_p()
+    assert N.lib().pbr_context_create(0, ctypes.byref(h)) == -2
+    assert not h.value
+
+
+def test_no_cpu_fallback_in_product_package():
+    """The product never imports the oracle (test infrastructure only)."""
+    pkg = os.path.join(ROOT, "physically_based_renderer_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                text = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in text and "from oracle" not in text, f
+                assert "liboracle" not in text and "pbr_oracle" not in text, f

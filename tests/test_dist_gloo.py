@@ -1,0 +1,80 @@
+"""The multi-GPU row-band path at world_size 2 (and 3) over gloo on CPU.
+
+Each rank fills only its own rows with the product's host fill, "shades" them, and the product's
+BandGather assembles the frame on rank 0; the result must equal a single-process frame bit for bit.
+With no GPU here the per-band shading is the CPU oracle -- this test covers the partition, the fill
+and the gather; the GPU band kernel itself is covered by test_gpu_parity.py::test_row_band_equals_full_frame.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_band(cfg, band, pc, env):
+    from oracle import oracle as O
+    from physically_based_renderer_amd import scenes as S
+
+    planes, _ = S.fill_gbuffer_host(cfg, band.row_begin, band.row_end, n_threads=2)
+    ops = O.OraclePass(eye=tuple(pc.eye_pos_w), ambient=tuple(pc.ambient_light), fresnel_r0=tuple(pc.fresnel_r0),
+                       opacity=pc.opacity, n_point=pc.num_point_lights, ambient_mode=pc.ambient_mode)
+    return O.shade(list(planes), ops, pc.light_array(), env, n_threads=2)
+
+
+def _worker(rank, world, port, height, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from physically_based_renderer_amd import dist as D
+    from physically_based_renderer_amd import scenes as S
+
+    D.init_from_env("gloo")
+    cfg = S.CONFIGS[3].with_size(72, height)
+    band = D.band_rows(cfg.height, world, rank)
+    pc = S.scene_pass(cfg)
+    rgba = _oracle_band(cfg, band, pc, S.env_map())
+    slot = torch.zeros((band.rows_max, cfg.width, 4), dtype=torch.float32)
+    slot[: band.rows] = torch.from_numpy(rgba)
+    g = D.BandGather(band, cfg.width, "cpu")
+    D.BandGather.wait(g.start(slot))
+    frame = g.assembled(cfg.height)
+    if rank == 0:
+        q.put(frame.numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,height", [(2, 40), (3, 37)])
+def test_row_bands_gather_equals_single_frame(world, height):
+    from physically_based_renderer_amd import dist as D
+    from physically_based_renderer_amd import scenes as S
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, height, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    cfg = S.CONFIGS[3].with_size(72, height)
+    whole = _oracle_band(cfg, D.band_rows(height, 1, 0), S.scene_pass(cfg), S.env_map())
+    assert frame.shape == whole.shape
+    assert np.array_equal(frame.view(np.uint32), whole.view(np.uint32))

@@ -183,3 +183,71 @@ def test_error_paths(gpu):
         ctx.set_pass(PassConstants(num_point_lights=N.PBR_MAX_LIGHTS + 1,
                                    lights_array=np.zeros((N.PBR_MAX_LIGHTS + 1, 12), np.float32)))
     ctx.close()
+
+
+def adversarial_planes(rng, h, w):
+    """Values straddling every fast-path window edge: +-0, subnormals, 2^+-20, 2^+-60, 2^+-96,
+    huge, inf, NaN, mixed with ordinary scene values."""
+    def field(scale, n_special=0.08):
+        base = rng.uniform(-scale, scale, (h, w)).astype(np.float32)
+        m = rng.uniform(size=(h, w))
+        e = rng.integers(-140, 125, (h, w)).astype(np.float64)
+        wild = (np.sign(rng.uniform(-1, 1, (h, w))) * rng.uniform(1, 2, (h, w)) * np.exp2(e)).astype(np.float32)
+        base = np.where(m < 0.25, wild, base)
+        for k, v in enumerate([0.0, -0.0, np.inf, -np.inf, np.nan, 2.0 ** -20, 2.0 ** -21, 2.0 ** 20, 1.0, 1e-45]):
+            base = np.where((m >= 0.25 + k * n_special / 10) & (m < 0.25 + (k + 1) * n_special / 10),
+                            np.float32(v), base)
+        return base
+
+    p = np.zeros((15, h, w), np.float32)
+    for i in range(3):
+        p[i] = field(30.0)
+    n = rng.normal(size=(3, h, w))
+    n = (n / np.linalg.norm(n, axis=0)).astype(np.float32)
+    sel = rng.uniform(size=(h, w)) < 0.3
+    for i in range(3):
+        p[3 + i] = np.where(sel, field(2.0), n[i])
+    for i in range(6, 15):
+        p[i] = np.where(rng.uniform(size=(h, w)) < 0.3, field(1.5), rng.uniform(0, 1, (h, w))).astype(np.float32)
+    return p
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fast_path_is_bit_identical_to_exact_only(seed, shading_ctx, gpu, env_map):
+    """The exact fast division/sqrt path must reproduce the compiler's IEEE sequences bit for bit,
+    on ordinary and adversarial inputs, for every light type and both ambient modes."""
+    rng = np.random.default_rng(100 + seed)
+    h, w = 64, 256
+    if seed < 2:
+        cfg = S.CONFIGS[[3, 4][seed]].with_size(w, h)
+        p, _ = S.fill_gbuffer_host(cfg)
+        pc = S.scene_pass(cfg)
+        nd, npt, ns = pc.num_dir_lights, pc.num_point_lights, pc.num_spot_lights
+        L = pc.light_array()
+    else:
+        p = adversarial_planes(rng, h, w)
+        nd, npt, ns = 5, 40, 9
+        L = np.zeros((nd + npt + ns, 12), np.float32)
+        L[:, 0:3] = rng.uniform(0, 50, (len(L), 3))
+        L[:, 3] = rng.uniform(0, 64, len(L))
+        L[:, 4:7] = rng.normal(size=(len(L), 3))
+        L[:, 8:11] = rng.uniform(-40, 40, (len(L), 3))
+        wild = rng.uniform(size=(len(L), 3)) < 0.2
+        L[:, 8:11] = np.where(wild, (2.0 ** rng.integers(-30, 30, (len(L), 3))).astype(np.float32), L[:, 8:11])
+        L[:nd, 4:7] = np.where(rng.uniform(size=(nd, 3)) < 0.3, np.float32(0.0), L[:nd, 4:7])
+    for mode in (N.PBR_AMBIENT_CONSTANT, N.PBR_AMBIENT_IBL_DIFFUSE):
+        for flags in (0, N.PBR_FLAG_TILED_CULLING | N.PBR_FLAG_F0_PLANE):
+            pc = PassConstants(num_dir_lights=nd, num_point_lights=npt, num_spot_lights=ns, ambient_mode=mode,
+                               flags=flags, lights_array=L, eye_pos_w=(0.5, 1.0, -5.0))
+            fast = gpu_shade(shading_ctx, p, pc, env_map, gpu)
+            pc_exact = PassConstants(**{**pc.__dict__, "flags": flags | N.PBR_FLAG_EXACT_ONLY})
+            exact = gpu_shade(shading_ctx, p, pc_exact, env_map, gpu)
+            eq = O.bit_equal(fast, exact)
+            assert eq.all(), f"seed {seed} mode {mode} flags {flags}: {int((~eq).sum())} channels differ"
+            if seed >= 2 and mode == 0 and flags == 0:
+                ref = O.shade(list(p), O.OraclePass(eye=(0.5, 1.0, -5.0), n_dir=nd, n_point=npt, n_spot=ns),
+                              L, None, n_threads=8)
+                finite = np.isfinite(ref) & np.isfinite(fast)
+                e = O.rel_err(fast[finite], ref[finite])
+                print(f"adversarial seed {seed}: max_rel (finite) {e.max():.3g}, "
+                      f"nan-pattern agreement {np.mean(np.isnan(fast) == np.isnan(ref)):.6f}")

@@ -1,0 +1,135 @@
+"""Host-side logic: G-buffer fill determinism and partition independence, scene constants,
+env-map ingest, row-band partitioning."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from physically_based_renderer_amd import _native as N
+from physically_based_renderer_amd import dist as D
+from physically_based_renderer_amd import envmap
+from physically_based_renderer_amd import scenes as S
+
+
+@pytest.mark.parametrize("cid", [1, 2, 3, 4, 5])
+def test_fill_is_partition_independent(cid):
+    cfg = S.CONFIGS[cid].with_size(200, 48) if cid != 1 else S.CONFIGS[1]
+    full, cov = S.fill_gbuffer_host(cfg, n_threads=3)
+    parts = [S.fill_gbuffer_host(cfg, r0, r1, n_threads=2)[0] for r0, r1 in [(0, 7), (7, 30), (30, cfg.height)]]
+    assert np.array_equal(np.concatenate(parts, axis=1).view(np.uint32), full.view(np.uint32))
+    again, cov2 = S.fill_gbuffer_host(cfg, n_threads=1)
+    assert np.array_equal(again.view(np.uint32), full.view(np.uint32)) and cov == cov2
+    assert np.isfinite(full).all()
+
+
+def test_random_covered_ranges():
+    cfg = S.CONFIGS[2].with_size(256, 64)
+    p, cov = S.fill_gbuffer_host(cfg)
+    assert cov == 256 * 64
+    assert p[0].min() >= -10 and p[0].max() < 10 and p[2].min() >= 0 and p[2].max() < 10
+    nl = np.sqrt((p[3:6].astype(np.float64) ** 2).sum(0))
+    assert np.allclose(nl, 1.0, atol=1e-6)
+    assert (p[9] >= 0).all() and (p[9] <= 1).all() and (p[11] == 1).all()
+    # F0 plane = lerp(0.04, albedo, metallic) in fp32 (Default.hlsl:94-95)
+    f0 = np.float32(0.04) + p[9] * (p[6] - np.float32(0.04))
+    assert np.array_equal(f0.view(np.uint32), p[12].view(np.uint32))
+
+
+def test_sphere_scene_coverage_and_normals():
+    p, cov = S.fill_gbuffer_host(S.CONFIGS[1])
+    hit = p[6] > 0  # background albedo is 0
+    assert cov == int(hit.sum()) and 10000 < cov < 15000
+    r = np.sqrt((p[0:3, hit].astype(np.float64) ** 2).sum(0))
+    assert np.allclose(r, 1.0, atol=1e-5)
+    assert (p[2, hit] < 0).all()  # the visible hemisphere faces the eye at z = -5
+
+
+def test_plane_scene_uses_all_materials():
+    cfg = S.CONFIGS[4].with_size(1024, 512)
+    p, _ = S.fill_gbuffer_host(cfg)
+    assert (p[1] == 0).all()
+    assert abs(p[2].max() - 500) < 1 and abs(p[2].min() + 500) < 1
+    assert len(np.unique(p[6][::64, ::64])) >= 5
+    assert (p[9] > 0).any()  # metal_bare metalness map
+
+
+@pytest.mark.parametrize("cid,n", [(1, 1), (2, 8), (3, 64), (4, 256), (5, 64)])
+def test_scene_pass(cid, n):
+    pc = S.scene_pass(S.CONFIGS[cid])
+    assert pc.num_point_lights == n and pc.num_dir_lights == 0 and pc.num_spot_lights == 0
+    L = pc.light_array()
+    assert L.shape == (n, 12)
+    assert np.allclose(pc.ambient_light, 0.03) and np.allclose(pc.fresnel_r0, 0.04) and pc.opacity == 1.0
+    if cid in (2, 3, 5):
+        assert (np.abs(L[:, 8:10]) <= 20).all() and (L[:, 10] <= 0).all() and (L[:, 0:3] < 100).all()
+    if cid == 1:
+        assert L[0, 8:11].tolist() == [20.0, 20.0, -20.0] and L[0, 0] == 100.0
+    assert pc.ambient_mode == S.CONFIGS[cid].ambient_mode
+
+
+def test_fill_rejects_bad_arguments():
+    cfg = S.CONFIGS[2].with_size(16, 16)
+    with pytest.raises(N.PbrError):
+        S.fill_gbuffer_host(cfg, 10, 5)
+    with pytest.raises(N.PbrError):
+        S.fill_gbuffer_host(cfg, 0, 17)
+
+
+def test_env_png16_decode_matches_pil_8bit_and_survey_stats():
+    env = envmap.load_chelsea_stairs_env()
+    assert env.shape == (180, 360, 4) and env.dtype == np.uint16
+    assert (env[..., 3] == 65535).all()
+    assert env[..., :3].min() == 300 and env[..., :3].max() == 65535
+    try:
+        from PIL import Image
+    except ImportError:
+        pytest.skip("PIL absent")
+    p8 = np.asarray(Image.open(envmap.CHELSEA_STAIRS_ENV))
+    assert np.array_equal(p8.astype(np.uint16), env[..., :3] >> 8)  # PIL truncates 16-bit to 8-bit
+
+
+def _png(w, h, depth, color, rows_bytes, filt):
+    import struct
+    import zlib
+
+    raw = b"".join(bytes([filt]) + r for r in rows_bytes)
+
+    def chunk(t, b):
+        return struct.pack(">I", len(b)) + t + b + struct.pack(">I", zlib.crc32(t + b) & 0xFFFFFFFF)
+
+    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, color, 0, 0, 0))
+            + chunk(b"IDAT", zlib.compress(raw)) + chunk(b"IEND", b""))
+
+
+def test_png_decoder_filters_and_formats():
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 65536, (5, 7, 3), dtype=np.uint16)
+    be = img.astype(">u2").tobytes()
+    rows = [be[i * 42:(i + 1) * 42] for i in range(5)]
+    dec = envmap.decode_png_rgba16(_png(7, 5, 16, 2, rows, 0))
+    assert np.array_equal(dec[..., :3], img) and (dec[..., 3] == 65535).all()
+    # Sub filter: encode row bytes as differences to the pixel 6 bytes to the left
+    sub_rows = []
+    for r in rows:
+        a = np.frombuffer(r, np.uint8).astype(np.int32)
+        d = a.copy()
+        d[6:] = (a[6:] - a[:-6]) & 0xFF
+        sub_rows.append(d.astype(np.uint8).tobytes())
+    assert np.array_equal(envmap.decode_png_rgba16(_png(7, 5, 16, 2, sub_rows, 1))[..., :3], img)
+    gray8 = rng.integers(0, 256, (3, 4), dtype=np.uint8)
+    g = envmap.decode_png_rgba16(_png(4, 3, 8, 0, [gray8[i].tobytes() for i in range(3)], 0))
+    assert np.array_equal(g[..., 0], gray8.astype(np.uint16) * 257) and np.array_equal(g[..., 0], g[..., 2])
+
+
+@pytest.mark.parametrize("height,world", [(8192, 8), (2160, 1), (2160, 2), (2160, 7), (100, 3), (8, 4), (0, 2)])
+def test_band_partition_covers_rows_once(height, world):
+    bands = D.all_bands(height, world)
+    assert bands[0].row_begin == 0 and bands[-1].row_end == height
+    for a, b in zip(bands, bands[1:]):
+        assert a.row_end == b.row_begin
+    for b in bands:
+        assert 0 <= b.rows <= b.rows_max
+        if b.row_end < height:
+            assert b.row_begin % 8 == 0 and b.row_end % 8 == 0
+    if height == 8192 and world == 8:
+        assert all(b.rows == 1024 for b in bands)
