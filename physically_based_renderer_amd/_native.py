@@ -10,7 +10,8 @@ import re
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "_lib", "libpbrshade.so")
+# PBR_LIB_PATH overrides the in-tree library (development A/B of kernel builds only).
+LIB_PATH = os.environ.get("PBR_LIB_PATH") or os.path.join(PKG_DIR, "_lib", "libpbrshade.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "pbr", "pbr_shade.h")
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
 

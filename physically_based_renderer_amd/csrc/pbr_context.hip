@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -32,6 +33,7 @@ struct pbr_context {
     uint32_t flags = 0;
     bool pass_set = false;
     unsigned long long* d_cull_stats = nullptr;
+    int pixels_per_thread = 2;  // kernel layout: packed pixel pairs (measured faster); PBR_PIXELS_PER_THREAD=1 overrides
     std::string last_error;
     std::mutex mu;
 };
@@ -90,6 +92,7 @@ int pbr_context_create(int device, pbr_context** out_ctx) {
     pbr_context* ctx = new (std::nothrow) pbr_context();
     if (!ctx) return PBR_ERR_OUT_OF_MEMORY;
     ctx->device = device;
+    if (const char* e = std::getenv("PBR_PIXELS_PER_THREAD")) ctx->pixels_per_thread = std::atoi(e) == 1 ? 1 : 2;
     DeviceGuard g(device);
     if (!g.ok) {
         delete ctx;
@@ -249,6 +252,9 @@ int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rg
     a.gb.width = gb->width;
     a.gb.height = gb->height;
     a.gb.row_stride = gb->row_stride;
+    a.gb.pairs_aligned = (gb->row_stride % 2) == 0;
+    for (int i = 0; i < 15; ++i)
+        if ((reinterpret_cast<uintptr_t>(a.gb.plane[i]) & 7u) != 0) a.gb.pairs_aligned = false;
     a.ps = ctx->pass;
     a.ps.env_w = ctx->env_w;
     a.ps.env_h = ctx->env_h;
@@ -262,6 +268,7 @@ int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rg
     a.apply_ao = apply_ao;
     a.cull = cull;
     a.exact_only = (ctx->flags & PBR_FLAG_EXACT_ONLY) != 0;
+    a.pixels_per_thread = ctx->pixels_per_thread;
     if ((reinterpret_cast<uintptr_t>(out_rgba) & 15u) != 0) return PBR_ERR_INVALID_ARGUMENT;  // float4 stores
 
     DeviceGuard g(ctx->device);

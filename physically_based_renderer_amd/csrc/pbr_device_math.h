@@ -31,22 +31,24 @@ __device__ __forceinline__ f3 normalize3(f3 v) {
 __device__ __forceinline__ float hlerp(float x, float y, float s) { return x + s * (y - x); }
 
 // ---- Exact fast paths --------------------------------------------------------------------------
-// With correctly rounded division/sqrt, hipcc expands x / y into
-//   v_div_scale(y), v_div_scale(x), r = v_rcp(y'), e = fma(-y', r, 1), r = fma(e, r, r),
-//   q = x' * r, t = fma(-y', q, x'), q = fma(t, r, q), t = fma(-y', q, x'), q = v_div_fmas(t, r, q),
-//   v_div_fixup(q, y, x)
-// and sqrt(x) into a scaled v_sqrt plus a +-1 ulp correction and a class fix-up. When the operands
-// lie in a window where the scale steps leave them unchanged and the fix-up has nothing to fix
-// (every operand and intermediate normal, no overflow), the sequences below are the SAME
-// operations on the same values, so they return bit-identical, correctly rounded results:
-//   div_nr:  0 < y in [2^-60, 2^60]; x == +-0, or |x| in [2^-96, 2^60] with |x / y| in
-//            [2^-120, 2^120] (so r, e, q and the residual t stay normal or exactly zero). The
-//            residual is formed as fma(y, q, -x) = -fma(-y, q, x), which for y > 0 also keeps the
-//            sign of a -0 numerator that the plain form loses before v_div_fixup restores it;
-//   sqrt_nr: x in [2^-96, 2^128), finite (no scaling, no class fix-up).
-// The light loop proves the window per pixel-light (PixelInvariants::fast_ok, the light's staged
-// flag and a few compares) and falls back to the compiler's full sequences otherwise; the
-// PBR_FLAG_EXACT_ONLY validation mode runs only the full sequences and must match bit for bit
+// With correctly rounded division, hipcc expands each x / y into ~11 operations (v_div_scale x2,
+// v_rcp, two Newton fma, three correction fma/mul, v_div_fmas, v_div_fixup) plus hazard NOPs; the
+// scale and fix-up steps exist for operands near the ends of the exponent range, zeros, infinities
+// and NaNs. Inside a window that excludes those cases the quotient is computed here as:
+//   y = recip_nr(b):  r = v_rcp(b); e = fma(-b, r, 1); y = fma(e, r, r)
+//       -- equals RN(1/b), the correctly rounded reciprocal, for EVERY significand at every exponent
+//          in [-64, 64] (exhaustive check on gfx950: tests/test_gpu_fastdiv.py);
+//   q = div_nr(a, y): q0 = a*y; t = fma(b, q0, -a); q = fma(-t, y, q0)
+//       -- Markstein's theorem: with y = RN(1/b), q0 within one ulp of a/b and the residual exact
+//          (fma), RN(q0 + (a - b q0) y) = RN(a/b). t is formed as -(a - b q0) so that a -0
+//          numerator keeps its sign for b > 0 (the plain form returns +0 there).
+// Window (proved per pixel-light by the callers, see fast_window_ok): 0 < b in [2^-60, 2^60];
+// a == +-0 or |a| in [2^-96, 2^60]; |a / b| in [2^-120, 2^120] (no overflow, no subnormal q0 or t).
+// One reciprocal serves every numerator with the same denominator (L/d, normalize, specular, /PI).
+// sqrt_nr replicates hipcc's correctly rounded sqrt (v_sqrt + a +-1 ulp correction) without its
+// scaling and class fix-up, exact for x in [2^-96, 2^128).
+// The light loop falls back to the compiler's full sequences whenever the window is not proved;
+// PBR_FLAG_EXACT_ONLY runs only those, and tests require both modes to agree bit for bit
 // (tests/test_gpu_parity.py::test_fast_path_is_bit_identical_to_exact_only).
 struct Recip {
     float y, r;
@@ -59,8 +61,6 @@ __device__ __forceinline__ Recip recip_nr(float y) {
 __device__ __forceinline__ float div_nr(float x, Recip d) {
     float q = x * d.r;
     float t = __builtin_fmaf(d.y, q, -x);
-    q = __builtin_fmaf(-t, d.r, q);
-    t = __builtin_fmaf(d.y, q, -x);
     return __builtin_fmaf(-t, d.r, q);
 }
 __device__ __forceinline__ float sqrt_nr(float x) {
@@ -103,6 +103,7 @@ struct PixelInvariants {
     float four_n_dot_v;     // 4.0f * max(dot(N,V), 0) (:95, left operand of the product)
     Recip r_pi;             // refined reciprocal of PI for the exact fast division by PI (:103)
     bool fast_ok;           // the pixel's inputs lie in the fast-path window (see below)
+    bool f0_nonzero;        // no F0 component is zero
 };
 
 // Per-pixel half of the fast-path proof ("exact fast path"). With every position
@@ -125,6 +126,9 @@ __device__ __forceinline__ bool fast_window_ok(f3 pos, f3 eye, f3 n, f3 albedo, 
     ok = ok && metallic >= 0.0f && metallic <= 1.0f && roughness >= 0.0f && roughness <= 1.0f;
     return ok;
 }
+
+// F0 with no zero component: then F = F0 + (1-F0) p stays >= 2^-20 for any p (see brdf checks).
+__device__ __forceinline__ bool f0_nonzero(f3 f0) { return f0.x != 0.0f && f0.y != 0.0f && f0.z != 0.0f; }
 
 // Per-light half, evaluated once when the light is staged: point/spot positions like pixel
 // positions; directional L = -Direction components zero or [2^-20, 16].
@@ -156,6 +160,7 @@ __device__ __forceinline__ PixelInvariants make_invariants(f3 n, f3 v, f3 albedo
     q.four_n_dot_v = 4.0f * n_dot_v;
     q.r_pi = recip_nr(kPi);
     q.fast_ok = false;
+    q.f0_nonzero = f0_nonzero(f0);
     return q;
 }
 
@@ -194,8 +199,10 @@ __device__ __forceinline__ f3 brdf_cook_torrance(const PixelInvariants& q, f3 ra
     float denom = q.four_n_dot_v * n_dot_l + 0.001f;
     f3 nom = mk3(ndf_g * f.x, ndf_g * f.y, ndf_g * f.z);
     if (FAST) {
-        ok = ok && zero_or_in(nom.x, 0x1p-60f, 0x1p60f) && zero_or_in(nom.y, 0x1p-60f, 0x1p60f) &&
-             zero_or_in(nom.z, 0x1p-60f, 0x1p60f) && denom <= 0x1p60f;
+        // F components are 0 or in [2^-40, 2^11] (F0 window; p == 0 or >= 2^-40 unless F0 has no
+        // zero), so nom = NDF*G*F is 0 or in [2^-70, 2^51] when NDF*G is 0 or in [2^-30, 2^40];
+        // denom is in [0.001, 2^17] by the pixel and light windows.
+        ok = ok && zero_or_in(ndf_g, 0x1p-30f, 0x1p40f) && (q.f0_nonzero || p == 0.0f || p >= 0x1p-40f);
     }
     const Recip rdenom = qrecip<FAST>(denom);
     f3 spec = mk3(qdiv<FAST>(nom.x, rdenom), qdiv<FAST>(nom.y, rdenom), qdiv<FAST>(nom.z, rdenom));
@@ -212,7 +219,7 @@ template <bool FAST>
 __device__ __forceinline__ f3 normalize_q(f3 v, bool& ok) {
     if (!FAST) return normalize3(v);
     float s = sqrt_nr(dot3(v, v));
-    ok = ok && s >= 0x1p-30f && s <= 0x1p30f;
+    ok = ok && s >= 0x1p-30f;  // s <= 1 + |L| <= 29 by the windows
     const Recip r = recip_nr(s);
     return mk3(div_nr(v.x, r), div_nr(v.y, r), div_nr(v.z, r));
 }

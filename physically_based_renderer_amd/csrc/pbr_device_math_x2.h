@@ -1,0 +1,184 @@
+// pbr_device_math_x2.h -- the exact fast path of pbr_device_math.h for a PAIR of pixels per
+// work-item, in packed fp32 (gfx950 v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32).
+//
+// Every operation is the scalar fast path's operation applied element-wise: a packed instruction
+// rounds each element exactly like its scalar form, so each pixel of the pair gets the bits the
+// scalar fast path (and therefore the compiler's full IEEE sequences) would give it. Transcendental
+// seeds (v_rcp_f32, v_sqrt_f32), compares, selects and the fp64 pow5 have no packed form and run
+// per element. Pixels that leave the fast-path window are re-evaluated by the scalar exact path.
+#pragma once
+#include "pbr_device_math.h"
+
+namespace pbr {
+
+typedef float v2 __attribute__((ext_vector_type(2)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+struct f3x2 {
+    v2 x, y, z;
+};
+
+__device__ __forceinline__ v2 vfma(v2 a, v2 b, v2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ v2 vmax(v2 a, v2 b) { return __builtin_elementwise_max(a, b); }  // IEEE maxNum
+__device__ __forceinline__ v2 vmin(v2 a, v2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ v2 vsat(v2 a) { return vmin(vmax(a, (v2)(0.0f)), (v2)(1.0f)); }
+__device__ __forceinline__ v2 vsel(v2i m, v2 a, v2 b) { return v2{m.x ? a.x : b.x, m.y ? a.y : b.y}; }
+__device__ __forceinline__ f3x2 add3(f3x2 a, f3x2 b) { return f3x2{a.x + b.x, a.y + b.y, a.z + b.z}; }
+// HLSL dot, same association as dot3: (a.x*b.x + a.y*b.y) + a.z*b.z
+__device__ __forceinline__ v2 dot3(f3x2 a, f3x2 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ v2 splat(float s) { return (v2)(s); }
+__device__ __forceinline__ f3x2 splat3(float x, float y, float z) { return f3x2{splat(x), splat(y), splat(z)}; }
+__device__ __forceinline__ f3 lane(const f3x2& v, int i) { return i ? mk3(v.x.y, v.y.y, v.z.y) : mk3(v.x.x, v.y.x, v.z.x); }
+
+struct Recip2 {
+    v2 y, r;
+};
+__device__ __forceinline__ Recip2 recip_nr(v2 y) {
+    v2 r = v2{__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)};
+    v2 e = vfma(-y, r, splat(1.0f));
+    return Recip2{y, vfma(e, r, r)};
+}
+__device__ __forceinline__ v2 div_nr(v2 x, Recip2 d) {  // Markstein step, see pbr_device_math.h
+    v2 q = x * d.r;
+    v2 t = vfma(d.y, q, -x);
+    return vfma(-t, d.r, q);
+}
+__device__ __forceinline__ v2 sqrt_nr(v2 x) {
+    v2 s = v2{__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+    v2i si = __builtin_bit_cast(v2i, s);
+    v2 sm = __builtin_bit_cast(v2, si - 1);
+    v2 sp = __builtin_bit_cast(v2, si + 1);
+    v2 rm = vfma(-sm, s, x);
+    v2 rp = vfma(-sp, s, x);
+    s = vsel(rm <= 0.0f, sm, s);
+    return vsel(rp > 0.0f, sp, s);
+}
+__device__ __forceinline__ v2 pow5(v2 x) { return v2{pow5(x.x), pow5(x.y)}; }
+// |x| in [lo, hi] per element (false for NaN), as an int mask (-1 / 0).
+__device__ __forceinline__ v2i in_win(v2 x, float lo, float hi) {
+    v2 a = __builtin_elementwise_abs(x);
+    return (a >= lo) & (a <= hi);
+}
+
+struct PixelInvariants2 {
+    f3x2 n, v, albedo, f0, one_minus_f0;
+    v2 one_minus_metal, a_sqr, a_sqr_minus_1, k, one_minus_k, ggx_v, four_n_dot_v;
+    v2i f0_nonzero;  // -1 where no F0 component is zero
+};
+
+// make_invariants (pbr_device_math.h) element-wise for the pair: the same operations, packed.
+__device__ __forceinline__ PixelInvariants2 make_invariants(const f3x2& n, const f3x2& v, const f3x2& albedo,
+                                                            const f3x2& f0, v2 metallic, v2 roughness) {
+    PixelInvariants2 q;
+    q.n = n;
+    q.v = v;
+    q.albedo = albedo;
+    q.f0 = f0;
+    q.one_minus_f0 = f3x2{1.0f - f0.x, 1.0f - f0.y, 1.0f - f0.z};
+    q.one_minus_metal = 1.0f - metallic;
+    v2 r = vmax(roughness, splat(0.05f));
+    v2 a = r * r;
+    q.a_sqr = a * a;
+    q.a_sqr_minus_1 = q.a_sqr - 1.0f;
+    v2 rr = (roughness + 1.0f);
+    q.k = (rr * rr) * 0.125f;  // (r*r) / 8.0f: division by a power of two is this exact product
+    q.one_minus_k = 1.0f - q.k;
+    v2 n_dot_v = vmax(dot3(n, v), splat(0.0f));
+    q.ggx_v = n_dot_v / (n_dot_v * q.one_minus_k + q.k);  // IEEE division per element
+    q.four_n_dot_v = 4.0f * n_dot_v;
+    q.f0_nonzero = (f0.x != 0.0f) & (f0.y != 0.0f) & (f0.z != 0.0f);
+    return q;
+}
+
+// normalize3 (IEEE sqrtf and division) on each element of the pair.
+__device__ __forceinline__ f3x2 normalize_ieee(const f3x2& v) {
+    const f3 a = normalize3(lane(v, 0)), b = normalize3(lane(v, 1));
+    return f3x2{v2{a.x, b.x}, v2{a.y, b.y}, v2{a.z, b.z}};
+}
+
+// Scalar PixelInvariants of pixel i of the pair (for the exact fallback).
+__device__ __forceinline__ PixelInvariants unpack_invariants(const PixelInvariants2& q, int i) {
+    PixelInvariants s;
+    s.n = lane(q.n, i);
+    s.v = lane(q.v, i);
+    s.albedo = lane(q.albedo, i);
+    s.f0 = lane(q.f0, i);
+    s.one_minus_f0 = lane(q.one_minus_f0, i);
+    s.one_minus_metal = i ? q.one_minus_metal.y : q.one_minus_metal.x;
+    s.a_sqr = i ? q.a_sqr.y : q.a_sqr.x;
+    s.a_sqr_minus_1 = i ? q.a_sqr_minus_1.y : q.a_sqr_minus_1.x;
+    s.k = i ? q.k.y : q.k.x;
+    s.one_minus_k = i ? q.one_minus_k.y : q.one_minus_k.x;
+    s.ggx_v = i ? q.ggx_v.y : q.ggx_v.x;
+    s.four_n_dot_v = i ? q.four_n_dot_v.y : q.four_n_dot_v.x;
+    s.r_pi = recip_nr(kPi);
+    s.fast_ok = false;
+    s.f0_nonzero = (i ? q.f0_nonzero.y : q.f0_nonzero.x) != 0;
+    return s;
+}
+
+// BRDFCookTorrance, packed fast path (scalar twin: brdf_cook_torrance<true>). `ok` collects the
+// per-iteration window conditions (see pbr_device_math.h).
+__device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, const Recip2& rpi, f3x2 radiance, f3x2 l, f3x2 h,
+                                        v2i& ok) {
+    v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
+    v2 n_dot_h_sqr = n_dot_h * n_dot_h;
+    v2 den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
+    den = kPi * den * den;
+    ok &= (den >= 0x1p-60f) & (den <= 0x1p60f);
+    v2 ndf = div_nr(q.a_sqr, recip_nr(den));
+    v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
+    v2 ggx_l = div_nr(n_dot_l, recip_nr(n_dot_l * q.one_minus_k + q.k));
+    v2 g = ggx_l * q.ggx_v;
+    v2 cos_theta = vsat(dot3(h, q.v));
+    v2 p = pow5(1.0f - cos_theta);
+    f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
+    v2 ndf_g = ndf * g;
+    v2 denom = q.four_n_dot_v * n_dot_l + 0.001f;
+    f3x2 nom = f3x2{ndf_g * f.x, ndf_g * f.y, ndf_g * f.z};
+    ok &= ((ndf_g == 0.0f) | in_win(ndf_g, 0x1p-30f, 0x1p40f)) & (q.f0_nonzero | (p == 0.0f) | (p >= 0x1p-40f));
+    const Recip2 rd = recip_nr(denom);
+    f3x2 spec = f3x2{div_nr(nom.x, rd), div_nr(nom.y, rd), div_nr(nom.z, rd)};
+    f3x2 kd = f3x2{(1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal};
+    return f3x2{((div_nr(kd.x * q.albedo.x, rpi) + spec.x) * radiance.x) * n_dot_l,
+                ((div_nr(kd.y * q.albedo.y, rpi) + spec.y) * radiance.y) * n_dot_l,
+                ((div_nr(kd.z * q.albedo.z, rpi) + spec.z) * radiance.z) * n_dot_l};
+}
+
+__device__ __forceinline__ f3x2 normalize_x2(f3x2 v, v2i& ok) {
+    v2 s = sqrt_nr(dot3(v, v));
+    ok &= (s >= 0x1p-30f);  // s <= 1 + |L| <= 29 by the windows
+    const Recip2 r = recip_nr(s);
+    return f3x2{div_nr(v.x, r), div_nr(v.y, r), div_nr(v.z, r)};
+}
+
+// ComputeDirectionalLight, packed fast path.
+__device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, const Recip2& rpi, float4 s, float4 d,
+                                               v2i& ok) {
+    f3x2 l = splat3(-d.x, -d.y, -d.z);
+    f3x2 h = normalize_x2(add3(q.v, l), ok);
+    return brdf_x2(q, rpi, splat3(s.x, s.y, s.z), l, h, ok);
+}
+
+// ComputePointLight / ComputeSpotLight, packed fast path. `lit` = the range test passed (exact,
+// as in the scalar version). Lanes with lit == 0 carry garbage in `out` and are never added.
+template <bool SPOT>
+__device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const Recip2& rpi, const f3x2& pos,
+                                                 float4 s, float4 d, float4 p, v2i& lit, v2i& ok) {
+    f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
+    v2 dist = sqrt_nr(dot3(l, l));
+    lit = !(dist > kLightRange);
+    ok &= (dist >= 0x1p-20f);
+    const Recip2 rdist = recip_nr(dist);
+    l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
+    f3x2 h = normalize_x2(add3(q.v, l), ok);
+    v2 dsat = vmax(dist, splat(0.01f));
+    v2 att = div_nr(splat(1.0f), recip_nr(dsat * dsat));
+    if (SPOT) {
+        v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
+        att *= v2{powf(c.x, s.w), powf(c.y, s.w)};
+    }
+    return brdf_x2(q, rpi, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
+}
+
+}  // namespace pbr

@@ -15,6 +15,7 @@ struct GBufferArgs {
     const float* plane[15];
     int width, height;
     int64_t row_stride;
+    bool pairs_aligned;  // every read plane 8-byte aligned and row_stride even: 8-byte pair loads
 };
 
 // Pass constants passed by value as kernel arguments (the shading subset of cbPass / cbMaterial).
@@ -38,6 +39,7 @@ struct LaunchArgs {
     int ambient_mode;
     bool f0_plane, apply_ao, cull;
     bool exact_only;  // PBR_FLAG_EXACT_ONLY: skip the exact fast path (validation mode)
+    int pixels_per_thread;  // 1 (32x8 tiles) or 2 (64x8 tiles, packed pairs)
 };
 
 hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);

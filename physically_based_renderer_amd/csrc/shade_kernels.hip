@@ -1,39 +1,53 @@
 // shade_kernels.hip -- gfx950 kernels for the G-buffer shading hot path.
 //
-// One workgroup = one 32x8-pixel screen tile = 256 work-items = 4 wave64s; wave w owns tile rows
-// 2w and 2w+1, so every per-plane load is two fully used 128-byte row segments and every RGBA
-// store is two 512-byte segments. The light list is staged through LDS in chunks of 256 lights
-// (3 float4 per light = the reference's 48-byte `Light`, LightingUtil.hlsl:9-17); every lane reads
-// the same LDS address in the light loop (broadcast, conflict-free).
+// One workgroup = one 64x8-pixel screen tile = 256 work-items = 4 wave64s. Work-item t shades the
+// horizontal pixel pair (2*(t%32), 2*(t%32)+1) of tile row t/32, so wave w owns tile rows 2w, 2w+1:
+// each plane load is one 8-byte load per lane (two full 256-byte row segments per wave) and each
+// pair of RGBA stores covers two 1-KiB row segments. The pair is shaded in packed fp32
+// (pbr_device_math_x2.h): every light-loop operation except the transcendental seeds and compares
+// issues once for both pixels.
 //
-// Tiled culling (PBR_FLAG_TILED_CULLING): the tile's world-space AABB comes from wave64
-// min/max shuffles plus a 4-entry LDS combine; each chunk's point/spot lights are range-tested
-// against it, one light per work-item, and compacted IN ORDER into LDS with a 64-bit ballot +
-// mbcnt prefix. A light is dropped only when it is provably beyond the 100-unit range of every
-// pixel of the tile, so the reference loop (LightingUtil.hlsl:131) would have added +0 for it:
-// the culled result is bit-identical to the unculled one.
+// The light list is staged through LDS in chunks of 256 lights (3 float4 per light = the reference's
+// 48-byte `Light`, LightingUtil.hlsl:9-17); every lane reads the same LDS record (broadcast).
+//
+// Tiled culling (PBR_FLAG_TILED_CULLING): the tile's world-space AABB comes from wave64 min/max
+// shuffles plus a 4-entry LDS combine; each chunk's point/spot lights are range-tested against it,
+// one light per work-item, and compacted IN ORDER into LDS with a 64-bit ballot + mbcnt prefix. A
+// light is dropped only when it is provably beyond the 100-unit range of every pixel of the tile, so
+// the reference loop (LightingUtil.hlsl:131) would have added +0 for it: the culled result is
+// bit-identical to the unculled one.
+//
+// Exact fallback: a pixel whose inputs or intermediates leave the fast-path window for any light is
+// flagged; after the fast loop, a block with any flagged pixel re-runs the light loop for those
+// pixels with the compiler's full IEEE sequences (scalar, pbr_device_math.h), replacing their sums.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 #include "pbr_device_math.h"
+#include "pbr_device_math_x2.h"
 #include "shade_kernels.h"
 
 namespace pbr {
 
 namespace {
 
-constexpr int kTileW = 32;
+constexpr int kTileW = 64;  // pixels; 32 work-items x 2 pixels
+#ifndef PBR_X2_LIGHT_UNROLL
+#define PBR_X2_LIGHT_UNROLL 1
+#endif
+#ifndef PBR_X2_MIN_WAVES
+#define PBR_X2_MIN_WAVES 4  // waves per SIMD the packed kernel is register-allocated for
+#endif
 constexpr int kTileH = 8;
-constexpr int kBlock = kTileW * kTileH;  // 256
-constexpr int kChunk = 256;              // lights staged per LDS pass
+constexpr int kBlock = 256;
+constexpr int kChunk = 256;  // lights staged per LDS pass
 // Conservative cull radius: d_fp32 >= d_true * (1 - 4.8e-7) (three roundings in L, three in the
 // dot, one in sqrt); a margin of 1e-4 relative covers that and the fp32 box-distance error.
 constexpr float kCullRadius = 100.01f;
 
 struct TileBounds {
     float mn[3], mx[3];
-    bool all_finite;
 };
 
 __device__ __forceinline__ float wave_min(float v) {
@@ -47,14 +61,19 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+struct Lds {
+    float4 light[3 * kChunk];
+    int wave_cnt[kBlock / 64];
+    float bounds[kBlock / 64][6];
+};
+
 // Stage lights [begin, begin+count) of the global list into LDS, culled against the tile when CULL.
 // Returns the number staged (identical in every work-item). Caller brackets with barriers.
 // Each staged record is the 48-byte Light with its unused pad1 (.w of the position float4)
 // replaced by the light's fast-path window flag (pbr_device_math.h, light_window_ok).
 template <bool CULL>
-__device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, int begin, int count, float4* s_light,
-                                           int* s_wave_cnt, const TileBounds& tb, bool cull_enabled,
-                                           bool directional) {
+__device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, int begin, int count, Lds& s,
+                                           const TileBounds& tb, bool cull_enabled, bool directional) {
     const int tid = threadIdx.x;
     const bool have = tid < count;
     float4 l0 = make_float4(0.f, 0.f, 0.f, 0.f), l1 = l0, l2 = l0;
@@ -67,9 +86,9 @@ __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, in
     }
     if (!CULL) {
         if (have) {
-            s_light[3 * tid + 0] = l0;
-            s_light[3 * tid + 1] = l1;
-            s_light[3 * tid + 2] = l2;
+            s.light[3 * tid + 0] = l0;
+            s.light[3 * tid + 1] = l1;
+            s.light[3 * tid + 2] = l2;
         }
         return count;
     }
@@ -83,84 +102,371 @@ __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, in
     const uint64_t mask = __ballot(keep);
     const int lane = tid & 63, wave = tid >> 6;
     const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-    if (lane == 0) s_wave_cnt[wave] = __popcll(mask);
+    if (lane == 0) s.wave_cnt[wave] = __popcll(mask);
     __syncthreads();
     int off = 0, total = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) {
-        const int c = s_wave_cnt[w];
+        const int c = s.wave_cnt[w];
         off += (w < wave) ? c : 0;
         total += c;
     }
     if (keep) {
         const int slot = off + before;
-        s_light[3 * slot + 0] = l0;
-        s_light[3 * slot + 1] = l1;
-        s_light[3 * slot + 2] = l2;
+        s.light[3 * slot + 0] = l0;
+        s.light[3 * slot + 1] = l1;
+        s.light[3 * slot + 2] = l2;
     }
     return total;
 }
 
-// One light's term of ComputeLighting: the exact fast path for every lane, then -- only if some lane
-// of the wave left the fast-path window -- the compiler's full IEEE sequences for those lanes. Both
-// produce the same bits wherever the fast path is taken, so the sum is independent of the choice.
-template <int KIND>  // 0 directional, 1 point, 2 spot
-__device__ __forceinline__ void accumulate_light(const PixelInvariants& q, f3 pos, const float4* rec, f3& direct) {
-    const float4 a = rec[0], b = rec[1], c = rec[2];
-    f3 col;
-    bool ok = q.fast_ok && c.w != 0.0f;
-    bool lit = true;
-    if (KIND == 0) col = directional_light<true>(q, a, b, ok);
-    else lit = point_or_spot_light<KIND == 2, true>(q, pos, a, b, c, col, ok);
-    if (__any(!ok)) {
-        if (!ok) {
-            bool unused = true;
-            if (KIND == 0) col = directional_light<false>(q, a, b, unused);
-            else lit = point_or_spot_light<KIND == 2, false>(q, pos, a, b, c, col, unused);
+// ComputeLighting (LightingUtil.hlsl:170-200) for both pixels of the pair on the packed fast path:
+// in-order sum from +0; `redo` collects pixels that left the fast-path window for a lit light.
+template <bool CULL>
+__device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, v2i fast_ok,
+                                              const float4* __restrict__ lights, const PassArgs& ps, Lds& s,
+                                              const TileBounds& tb, bool cull_enabled, v2i& redo, int& kept_total) {
+    const Recip2 rpi = recip_nr(splat(kPi));
+    f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
+    for (int base = 0; base < ps.n_dir; base += kChunk) {  // directional: never culled
+        const int cnt = min(kChunk, ps.n_dir - base);
+        __syncthreads();
+        stage_chunk<false>(lights, base, cnt, s, tb, false, true);
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {
+            const float4* r = &s.light[3 * j];
+            v2i ok = fast_ok & (r[2].w != 0.0f ? -1 : 0);
+            const f3x2 c = directional_x2(q, rpi, r[0], r[1], ok);
+            redo |= ~ok;
+            direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
         }
     }
-    if (lit) direct = add3(direct, col);
+    const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
+#pragma unroll 1
+    for (int kind = 1; kind <= 2; ++kind) {
+        const int b0 = kind == 1 ? pt_begin : sp_begin, b1 = kind == 1 ? sp_begin : end;
+        for (int base = b0; base < b1; base += kChunk) {
+            const int cnt = min(kChunk, b1 - base);
+            __syncthreads();
+            const int kept = stage_chunk<CULL>(lights, base, cnt, s, tb, cull_enabled, false);
+            __syncthreads();
+            kept_total += kept;
+            // PBR_X2_LIGHT_UNROLL > 1 lets the scheduler interleave lights (measured: no gain, the
+            // loop is VALU-throughput bound, not wait-state bound).
+#pragma unroll PBR_X2_LIGHT_UNROLL
+            for (int j = 0; j < kept; ++j) {
+                const float4* r = &s.light[3 * j];
+                v2i ok = fast_ok & (r[2].w != 0.0f ? -1 : 0);
+                v2i lit;
+                const f3x2 c = kind == 1 ? point_or_spot_x2<false>(q, rpi, pos, r[0], r[1], r[2], lit, ok)
+                                         : point_or_spot_x2<true>(q, rpi, pos, r[0], r[1], r[2], lit, ok);
+                redo |= lit & ~ok;
+                // An unlit light adds +0 in the reference (identity on a sum that is never -0).
+                direct = add3(direct, f3x2{vsel(lit, c.x, splat(0.0f)), vsel(lit, c.y, splat(0.0f)),
+                                           vsel(lit, c.z, splat(0.0f))});
+            }
+        }
+    }
+    return direct;
+}
+
+// The same sum with the compiler's full IEEE sequences, for one pixel (the exact fallback and the
+// PBR_FLAG_EXACT_ONLY mode). Every work-item of the block must call it (it stages lights).
+template <bool CULL>
+__device__ __forceinline__ void lighting_exact(const PixelInvariants& qa, const PixelInvariants& qb, f3 pa, f3 pb,
+                                               bool need_a, bool need_b, const float4* __restrict__ lights,
+                                               const PassArgs& ps, Lds& s, const TileBounds& tb,
+                                               bool cull_enabled, f3& da, f3& db) {
+    da = mk3(0.0f, 0.0f, 0.0f);
+    db = mk3(0.0f, 0.0f, 0.0f);
+    bool unused = true;
+    for (int base = 0; base < ps.n_dir; base += kChunk) {
+        const int cnt = min(kChunk, ps.n_dir - base);
+        __syncthreads();
+        stage_chunk<false>(lights, base, cnt, s, tb, false, true);
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {
+            const float4* r = &s.light[3 * j];
+            if (need_a) da = add3(da, directional_light<false>(qa, r[0], r[1], unused));
+            if (need_b) db = add3(db, directional_light<false>(qb, r[0], r[1], unused));
+        }
+    }
+    const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
+#pragma unroll 1
+    for (int kind = 1; kind <= 2; ++kind) {
+        const int b0 = kind == 1 ? pt_begin : sp_begin, b1 = kind == 1 ? sp_begin : end;
+        for (int base = b0; base < b1; base += kChunk) {
+            const int cnt = min(kChunk, b1 - base);
+            __syncthreads();
+            const int kept = stage_chunk<CULL>(lights, base, cnt, s, tb, cull_enabled, false);
+            __syncthreads();
+            for (int j = 0; j < kept; ++j) {
+                const float4* r = &s.light[3 * j];
+                f3 c;
+                if (need_a) {
+                    const bool lit = kind == 1 ? point_or_spot_light<false, false>(qa, pa, r[0], r[1], r[2], c, unused)
+                                               : point_or_spot_light<true, false>(qa, pa, r[0], r[1], r[2], c, unused);
+                    if (lit) da = add3(da, c);
+                }
+                if (need_b) {
+                    const bool lit = kind == 1 ? point_or_spot_light<false, false>(qb, pb, r[0], r[1], r[2], c, unused)
+                                               : point_or_spot_light<true, false>(qb, pb, r[0], r[1], r[2], c, unused);
+                    if (lit) db = add3(db, c);
+                }
+            }
+        }
+    }
+}
+
+// The pair's G-buffer values in packed form: element 0 = pixel A, element 1 = pixel B.
+struct PairIn {
+    f3x2 pos, n, albedo, f0;
+    v2 metallic, roughness, ao;
+};
+
+template <bool F0_PLANE, bool APPLY_AO>
+__device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArgs& ps, int64_t ia, int64_t ib,
+                                            bool vector_load) {
+    v2 v[15];
+    if (vector_load) {  // both pixels exist and the pair is 8-byte aligned in every plane
+#pragma unroll
+        for (int i = 0; i < 15; ++i) {
+            if ((i == 11 && !APPLY_AO) || (i >= 12 && !F0_PLANE)) continue;
+            const float2 t = *reinterpret_cast<const float2*>(gb.plane[i] + ia);
+            v[i] = v2{t.x, t.y};
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 15; ++i) {
+            if ((i == 11 && !APPLY_AO) || (i >= 12 && !F0_PLANE)) continue;
+            v[i] = v2{gb.plane[i][ia], gb.plane[i][ib]};
+        }
+    }
+    PairIn p;
+    p.pos = f3x2{v[0], v[1], v[2]};
+    p.n = f3x2{v[3], v[4], v[5]};
+    p.albedo = f3x2{v[6], v[7], v[8]};
+    p.metallic = v[9];
+    p.roughness = v[10];
+    p.ao = APPLY_AO ? v[11] : splat(1.0f);
+    if (F0_PLANE) {  // Default.hlsl:92
+        p.f0 = f3x2{v[12], v[13], v[14]};
+    } else {  // F0 = lerp(g_FresnelR0, diffuseAlbedo, metallic)  (Default.hlsl:94-95): x + s*(y - x)
+        p.f0 = f3x2{ps.fresnel_r0[0] + p.metallic * (p.albedo.x - ps.fresnel_r0[0]),
+                    ps.fresnel_r0[1] + p.metallic * (p.albedo.y - ps.fresnel_r0[1]),
+                    ps.fresnel_r0[2] + p.metallic * (p.albedo.z - ps.fresnel_r0[2])};
+    }
+    return p;
+}
+
+// Ambient + tonemap + gamma for one pixel (Default.hlsl:139-160), returns the output RGBA.
+template <int AMBIENT, bool APPLY_AO>
+__device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float ao, f3 direct, const PassArgs& ps,
+                                               const float4* __restrict__ env) {
+    const PixelInvariants& q = p;
+    f3 ambient;
+    if (AMBIENT == kAmbientIblDiffuse) {
+        // Default.hlsl:141-146: kS = FresnelSchlick(N, V, F0); kD = (1 - kS)(1 - metallic);
+        // irradiance = env.Sample(linear-wrap, WorldToSkyUV(N)); ambient = kD * (irradiance * albedo)
+        const float cos_theta = hsat(dot3(p.n, q.v));
+        const float pw = pow5(1.0f - cos_theta);
+        const f3 ks = mk3(p.f0.x + q.one_minus_f0.x * pw, p.f0.y + q.one_minus_f0.y * pw, p.f0.z + q.one_minus_f0.z * pw);
+        const f3 kd = mk3((1.0f - ks.x) * q.one_minus_metal, (1.0f - ks.y) * q.one_minus_metal,
+                          (1.0f - ks.z) * q.one_minus_metal);
+        float su, sv;
+        world_to_sky_uv(p.n, su, sv);
+        const f3 irr = sample_linear_wrap(env, ps.env_w, ps.env_h, su, sv);
+        const f3 diffuse = mk3(irr.x * p.albedo.x, irr.y * p.albedo.y, irr.z * p.albedo.z);
+        ambient = mk3(kd.x * diffuse.x, kd.y * diffuse.y, kd.z * diffuse.z);
+    } else {
+        // g_AmbientLight * diffuseAlbedo  (Default.hlsl:150)
+        ambient = mk3(ps.ambient[0] * p.albedo.x, ps.ambient[1] * p.albedo.y, ps.ambient[2] * p.albedo.z);
+    }
+    if (APPLY_AO) ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
+    f3 lit = add3(ambient, direct);
+    lit = mk3(lit.x / (lit.x + 1.0f), lit.y / (lit.y + 1.0f), lit.z / (lit.z + 1.0f));  // Default.hlsl:153
+    return make_float4(powf(lit.x, kInvGamma), powf(lit.y, kInvGamma), powf(lit.z, kInvGamma), ps.opacity);
 }
 
 }  // namespace
 
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
-__global__ __launch_bounds__(kBlock) void shade_tile_kernel(GBufferArgs gb, PassArgs ps,
+__global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GBufferArgs gb, PassArgs ps,
                                                             const float4* __restrict__ lights,
                                                             const float4* __restrict__ env,
                                                             float4* __restrict__ out, int64_t out_stride,
                                                             unsigned long long* __restrict__ cull_stats,
                                                             bool exact_only) {
-    __shared__ float4 s_light[3 * kChunk];
-    __shared__ int s_wave_cnt[kBlock / 64];
-    __shared__ float s_bounds[kBlock / 64][6];
+    __shared__ Lds s;
 
     const int tid = threadIdx.x;
-    const int x = blockIdx.x * kTileW + (tid & (kTileW - 1));
-    const int y = blockIdx.y * kTileH + (tid / kTileW);
+    const int xa = blockIdx.x * kTileW + 2 * (tid & 31);
+    const int y = blockIdx.y * kTileH + (tid >> 5);
+    const bool va = (xa < gb.width) && (y < gb.height);
+    const bool vb = (xa + 1 < gb.width) && (y < gb.height);
+    const int64_t row = (int64_t)y * gb.row_stride;
+
+    const PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
+                                                   vb && gb.pairs_aligned);
+    const f3 pa = lane(p.pos, 0), pb = lane(p.pos, 1);
+
+    // V = normalize(g_CameraPosW - pin.PosW)  (Default.hlsl:53)
+    const f3 eye = mk3(ps.eye[0], ps.eye[1], ps.eye[2]);
+    const f3x2 v = normalize_ieee(f3x2{ps.eye[0] - p.pos.x, ps.eye[1] - p.pos.y, ps.eye[2] - p.pos.z});
+    const PixelInvariants2 q2 = make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness);
+    const bool ok_a = !exact_only && fast_window_ok(pa, eye, lane(p.n, 0), lane(p.albedo, 0), lane(p.f0, 0),
+                                                    p.metallic.x, p.roughness.x);
+    const bool ok_b = !exact_only && fast_window_ok(pb, eye, lane(p.n, 1), lane(p.albedo, 1), lane(p.f0, 1),
+                                                    p.metallic.y, p.roughness.y);
+
+    TileBounds tb{};
+    bool cull_enabled = false;
+    if (CULL) {
+        const bool finite = (!va || (isfinite(pa.x) && isfinite(pa.y) && isfinite(pa.z))) &&
+                            (!vb || (isfinite(pb.x) && isfinite(pb.y) && isfinite(pb.z)));
+        const float big = 3.0e38f;
+        float b[6];
+        b[0] = fminf(va ? pa.x : big, vb ? pb.x : big);
+        b[1] = fminf(va ? pa.y : big, vb ? pb.y : big);
+        b[2] = fminf(va ? pa.z : big, vb ? pb.z : big);
+        b[3] = fmaxf(va ? pa.x : -big, vb ? pb.x : -big);
+        b[4] = fmaxf(va ? pa.y : -big, vb ? pb.y : -big);
+        b[5] = fmaxf(va ? pa.z : -big, vb ? pb.z : -big);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) b[i] = wave_min(b[i]);
+#pragma unroll
+        for (int i = 3; i < 6; ++i) b[i] = wave_max(b[i]);
+        if ((tid & 63) == 0) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) s.bounds[tid >> 6][i] = b[i];
+        }
+        // Non-finite positions in the tile disable culling (the reference's NaN/inf behaviour at
+        // LightingUtil.hlsl:131 is then reproduced light by light).
+        cull_enabled = __syncthreads_and(finite) != 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            tb.mn[i] = fminf(fminf(s.bounds[0][i], s.bounds[1][i]), fminf(s.bounds[2][i], s.bounds[3][i]));
+            tb.mx[i] = fmaxf(fmaxf(s.bounds[0][i + 3], s.bounds[1][i + 3]), fmaxf(s.bounds[2][i + 3], s.bounds[3][i + 3]));
+        }
+    }
+
+    // ComputeLighting (LightingUtil.hlsl:170-200) on the packed fast path. From here on the pair
+    // lives only in packed form (q2, pos2); the scalar views are rebuilt from it afterwards so the
+    // loop does not carry two copies of the invariants.
+    int kept_total = 0;
+    v2i redo = v2i{0, 0};
+    const f3x2 pos2 = p.pos;
+    const float ao_a = p.ao.x, ao_b = p.ao.y;
+    const f3x2 d2 = lighting_fast<CULL>(q2, pos2, v2i{ok_a ? -1 : 0, ok_b ? -1 : 0}, lights, ps, s, tb, cull_enabled,
+                                        redo, kept_total);
+    const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
+    f3 da = lane(d2, 0), db = lane(d2, 1);
+    const bool need_a = va && redo.x != 0, need_b = vb && redo.y != 0;
+    if (__syncthreads_or(need_a || need_b)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
+        f3 ea, eb;
+        lighting_exact<CULL>(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, s, tb, cull_enabled,
+                             ea, eb);
+        if (need_a) da = ea;
+        if (need_b) db = eb;
+    }
+    if (CULL && tid == 0 && cull_stats != nullptr) {
+        atomicAdd(&cull_stats[0], (unsigned long long)kept_total);
+        atomicAdd(&cull_stats[1], 1ull);
+    }
+
+    float4* orow = out + (int64_t)y * out_stride;
+    if (va) orow[xa] = finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env);
+    if (vb) orow[xa + 1] = finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env);
+}
+
+// ---- One pixel per work-item (32x8 tiles) ---------------------------------------------------------
+// The same algorithm on the scalar fast path (pbr_device_math.h). Packing a pixel pair (above) halves
+// the instruction count but not the VALU cycles (a v_pk_fma_f32 issues in twice the cycles of a
+// v_fma_f32 on gfx950), and its register footprint costs a wave per SIMD; the launcher picks the
+// faster layout (PBR_PIXELS_PER_THREAD).
+namespace {
+
+constexpr int kTileW1 = 32;
+
+template <bool CULL>
+__device__ __forceinline__ f3 lighting_fast1(const PixelInvariants& q, f3 pos, const float4* __restrict__ lights,
+                                             const PassArgs& ps, Lds& s, const TileBounds& tb, bool cull_enabled,
+                                             bool& redo, int& kept_total) {
+    f3 direct = mk3(0.0f, 0.0f, 0.0f);
+    for (int base = 0; base < ps.n_dir; base += kChunk) {  // directional: never culled
+        const int cnt = min(kChunk, ps.n_dir - base);
+        __syncthreads();
+        stage_chunk<false>(lights, base, cnt, s, tb, false, true);
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {
+            const float4* r = &s.light[3 * j];
+            bool ok = q.fast_ok && r[2].w != 0.0f;
+            const f3 c = directional_light<true>(q, r[0], r[1], ok);
+            redo = redo || !ok;
+            direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
+        }
+    }
+    const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
+#pragma unroll 1
+    for (int kind = 1; kind <= 2; ++kind) {
+        const int b0 = kind == 1 ? pt_begin : sp_begin, b1 = kind == 1 ? sp_begin : end;
+        for (int base = b0; base < b1; base += kChunk) {
+            const int cnt = min(kChunk, b1 - base);
+            __syncthreads();
+            const int kept = stage_chunk<CULL>(lights, base, cnt, s, tb, cull_enabled, false);
+            __syncthreads();
+            kept_total += kept;
+            for (int j = 0; j < kept; ++j) {
+                const float4* r = &s.light[3 * j];
+                bool ok = q.fast_ok && r[2].w != 0.0f;
+                f3 c;
+                const bool lit = kind == 1 ? point_or_spot_light<false, true>(q, pos, r[0], r[1], r[2], c, ok)
+                                           : point_or_spot_light<true, true>(q, pos, r[0], r[1], r[2], c, ok);
+                if (lit) {  // an unlit light adds +0 in the reference: the identity on this sum
+                    redo = redo || !ok;
+                    direct = add3(direct, c);
+                }
+            }
+        }
+    }
+    return direct;
+}
+
+}  // namespace
+
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
+__global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, PassArgs ps,
+                                                             const float4* __restrict__ lights,
+                                                             const float4* __restrict__ env,
+                                                             float4* __restrict__ out, int64_t out_stride,
+                                                             unsigned long long* __restrict__ cull_stats,
+                                                             bool exact_only) {
+    __shared__ Lds s;
+    const int tid = threadIdx.x;
+    const int x = blockIdx.x * kTileW1 + (tid & (kTileW1 - 1));
+    const int y = blockIdx.y * kTileH + (tid / kTileW1);
     const bool valid = (x < gb.width) && (y < gb.height);
     const int64_t idx = valid ? (int64_t)y * gb.row_stride + x : 0;  // frames are never empty here
 
-    const f3 pos = mk3(gb.plane[0][idx], gb.plane[1][idx], gb.plane[2][idx]);
-    const f3 n = mk3(gb.plane[3][idx], gb.plane[4][idx], gb.plane[5][idx]);
-    const f3 albedo = mk3(gb.plane[6][idx], gb.plane[7][idx], gb.plane[8][idx]);
+    f3 pos, n, albedo, f0;
+    pos = mk3(gb.plane[0][idx], gb.plane[1][idx], gb.plane[2][idx]);
+    n = mk3(gb.plane[3][idx], gb.plane[4][idx], gb.plane[5][idx]);
+    albedo = mk3(gb.plane[6][idx], gb.plane[7][idx], gb.plane[8][idx]);
     const float metallic = gb.plane[9][idx];
     const float roughness = gb.plane[10][idx];
-
-    // V = normalize(g_CameraPosW - pin.PosW)  (Default.hlsl:53)
-    const f3 v = normalize3(mk3(ps.eye[0] - pos.x, ps.eye[1] - pos.y, ps.eye[2] - pos.z));
-    f3 f0;
+    const float ao = APPLY_AO ? gb.plane[11][idx] : 1.0f;
     if (F0_PLANE) {  // Default.hlsl:92
         f0 = mk3(gb.plane[12][idx], gb.plane[13][idx], gb.plane[14][idx]);
     } else {  // F0 = lerp(g_FresnelR0, diffuseAlbedo, metallic)  (Default.hlsl:94-95)
         f0 = mk3(hlerp(ps.fresnel_r0[0], albedo.x, metallic), hlerp(ps.fresnel_r0[1], albedo.y, metallic),
                  hlerp(ps.fresnel_r0[2], albedo.z, metallic));
     }
-    PixelInvariants q = make_invariants(n, v, albedo, f0, metallic, roughness);
-    q.fast_ok = !exact_only && fast_window_ok(pos, mk3(ps.eye[0], ps.eye[1], ps.eye[2]), n, albedo, f0, metallic,
-                                              roughness);
+    // V = normalize(g_CameraPosW - pin.PosW)  (Default.hlsl:53)
+    const f3 eye = mk3(ps.eye[0], ps.eye[1], ps.eye[2]);
+    PixelInvariants q = make_invariants(n, normalize3(sub3(eye, pos)), albedo, f0, metallic, roughness);
+    q.fast_ok = !exact_only && fast_window_ok(pos, eye, n, albedo, f0, metallic, roughness);
 
-    TileBounds tb;
+    TileBounds tb{};
     bool cull_enabled = false;
     if (CULL) {
         const bool finite = !valid || (isfinite(pos.x) && isfinite(pos.y) && isfinite(pos.z));
@@ -173,81 +479,30 @@ __global__ __launch_bounds__(kBlock) void shade_tile_kernel(GBufferArgs gb, Pass
         for (int i = 3; i < 6; ++i) b[i] = wave_max(b[i]);
         if ((tid & 63) == 0) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) s_bounds[tid >> 6][i] = b[i];
+            for (int i = 0; i < 6; ++i) s.bounds[tid >> 6][i] = b[i];
         }
-        // Non-finite positions in the tile disable culling (the reference's NaN/inf behaviour at
-        // LightingUtil.hlsl:131 is then reproduced light by light).
         cull_enabled = __syncthreads_and(finite) != 0;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            tb.mn[i] = fminf(fminf(s_bounds[0][i], s_bounds[1][i]), fminf(s_bounds[2][i], s_bounds[3][i]));
-            tb.mx[i] = fmaxf(fmaxf(s_bounds[0][i + 3], s_bounds[1][i + 3]), fmaxf(s_bounds[2][i + 3], s_bounds[3][i + 3]));
+            tb.mn[i] = fminf(fminf(s.bounds[0][i], s.bounds[1][i]), fminf(s.bounds[2][i], s.bounds[3][i]));
+            tb.mx[i] = fmaxf(fmaxf(s.bounds[0][i + 3], s.bounds[1][i + 3]), fmaxf(s.bounds[2][i + 3], s.bounds[3][i + 3]));
         }
     }
 
-    // ComputeLighting (LightingUtil.hlsl:170-200): in-order sum from +0.
-    f3 direct = mk3(0.0f, 0.0f, 0.0f);
     int kept_total = 0;
-
-    // Directional lights [0, n_dir): never culled (no range).
-    for (int base = 0; base < ps.n_dir; base += kChunk) {
-        const int cnt = min(kChunk, ps.n_dir - base);
-        __syncthreads();
-        stage_chunk<false>(lights, base, cnt, s_light, s_wave_cnt, tb, false, true);
-        __syncthreads();
-        for (int j = 0; j < cnt; ++j) accumulate_light<0>(q, pos, &s_light[3 * j], direct);
-    }
-    // Point lights [n_dir, n_dir + n_point), then spot lights.
-    const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
-    for (int base = pt_begin; base < sp_begin; base += kChunk) {
-        const int cnt = min(kChunk, sp_begin - base);
-        __syncthreads();
-        const int kept = stage_chunk<CULL>(lights, base, cnt, s_light, s_wave_cnt, tb, cull_enabled, false);
-        __syncthreads();
-        kept_total += kept;
-        for (int j = 0; j < kept; ++j) accumulate_light<1>(q, pos, &s_light[3 * j], direct);
-    }
-    for (int base = sp_begin; base < end; base += kChunk) {
-        const int cnt = min(kChunk, end - base);
-        __syncthreads();
-        const int kept = stage_chunk<CULL>(lights, base, cnt, s_light, s_wave_cnt, tb, cull_enabled, false);
-        __syncthreads();
-        kept_total += kept;
-        for (int j = 0; j < kept; ++j) accumulate_light<2>(q, pos, &s_light[3 * j], direct);
+    bool redo = false;
+    f3 direct = lighting_fast1<CULL>(q, pos, lights, ps, s, tb, cull_enabled, redo, kept_total);
+    const bool need = valid && redo;
+    if (__syncthreads_or(need)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
+        f3 e, unused;
+        lighting_exact<CULL>(q, q, pos, pos, need, false, lights, ps, s, tb, cull_enabled, e, unused);
+        if (need) direct = e;
     }
     if (CULL && tid == 0 && cull_stats != nullptr) {
         atomicAdd(&cull_stats[0], (unsigned long long)kept_total);
         atomicAdd(&cull_stats[1], 1ull);
     }
-
-    f3 ambient;
-    if (AMBIENT == kAmbientIblDiffuse) {
-        // Default.hlsl:141-146: kS = FresnelSchlick(N, V, F0); kD = (1 - kS)(1 - metallic);
-        // irradiance = env.Sample(linear-wrap, WorldToSkyUV(N)); ambient = kD * (irradiance * albedo)
-        const float cos_theta = hsat(dot3(n, v));
-        const float p = pow5(1.0f - cos_theta);
-        const f3 ks = mk3(f0.x + q.one_minus_f0.x * p, f0.y + q.one_minus_f0.y * p, f0.z + q.one_minus_f0.z * p);
-        const f3 kd = mk3((1.0f - ks.x) * q.one_minus_metal, (1.0f - ks.y) * q.one_minus_metal,
-                          (1.0f - ks.z) * q.one_minus_metal);
-        float su, sv;
-        world_to_sky_uv(n, su, sv);
-        const f3 irr = sample_linear_wrap(env, ps.env_w, ps.env_h, su, sv);
-        const f3 diffuse = mk3(irr.x * albedo.x, irr.y * albedo.y, irr.z * albedo.z);
-        ambient = mk3(kd.x * diffuse.x, kd.y * diffuse.y, kd.z * diffuse.z);
-    } else {
-        // g_AmbientLight * diffuseAlbedo  (Default.hlsl:150)
-        ambient = mk3(ps.ambient[0] * albedo.x, ps.ambient[1] * albedo.y, ps.ambient[2] * albedo.z);
-    }
-    if (APPLY_AO) {
-        const float ao = gb.plane[11][idx];
-        ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
-    }
-    f3 lit = add3(ambient, direct);
-    lit = mk3(lit.x / (lit.x + 1.0f), lit.y / (lit.y + 1.0f), lit.z / (lit.z + 1.0f));  // Default.hlsl:153
-    if (valid) {
-        out[(int64_t)y * out_stride + x] =
-            make_float4(powf(lit.x, kInvGamma), powf(lit.y, kInvGamma), powf(lit.z, kInvGamma), ps.opacity);
-    }
+    if (valid) out[(int64_t)y * out_stride + x] = finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env);
 }
 
 __global__ void decode_env_kernel(const uint16_t* __restrict__ src, float4* __restrict__ dst, int n) {
@@ -261,9 +516,15 @@ __global__ void decode_env_kernel(const uint16_t* __restrict__ src, float4* __re
 
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
-    dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream, a.gb,
-                       a.ps, a.lights, a.env, a.out, a.out_stride, a.cull_stats, a.exact_only);
+    if (a.pixels_per_thread == 2) {
+        dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
+        hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream, a.gb,
+                           a.ps, a.lights, a.env, a.out, a.out_stride, a.cull_stats, a.exact_only);
+    } else {
+        dim3 grid((a.gb.width + kTileW1 - 1) / kTileW1, (a.gb.height + kTileH - 1) / kTileH);
+        hipLaunchKernelGGL((shade_tile1_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,
+                           a.gb, a.ps, a.lights, a.env, a.out, a.out_stride, a.cull_stats, a.exact_only);
+    }
     return hipGetLastError();
 }
 
