@@ -110,17 +110,24 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=0, help="BASELINE config id (default 3 at N=1, 5 at N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (the benchmark); gloo = host-staged gather, for exercising the "
+                         "multi-rank path on one GPU")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="rows in the CPU-baseline sample (0 = the whole frame: ~1.5 s on 16 host threads)")
     args = ap.parse_args()
 
-    rank, world, local = D.init_from_env("nccl")
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    n_dev = torch.cuda.device_count()
+    local_env = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "nccl" and local_env >= n_dev:
+        raise SystemExit(f"LOCAL_RANK {local_env} but only {n_dev} visible GPU(s): RCCL needs one GPU per rank")
+    torch.cuda.set_device(local_env % n_dev)
+    rank, world, local = D.init_from_env(args.dist_backend)
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
+    device = torch.device("cuda", local % n_dev)
 
     cid = args.config or (3 if world == 1 else 5)
     cfg = S.CONFIGS[cid]
@@ -144,7 +151,7 @@ def main():
     from physically_based_renderer_amd.renderer import GBuffer
 
     gb = GBuffer(planes_dev)
-    ctx = ShadingContext(local)
+    ctx = ShadingContext(device.index)
     ctx.set_pass(pc)
     if env is not None:
         ctx.set_env_map(env)
@@ -190,7 +197,21 @@ def main():
     elapsed = time.perf_counter() - t_start
     kernel_ms = [a.elapsed_time(b) for a, b in events]
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    gather_ok = None
+    if world > 1:
+        # Property check of the assembled image: each rank's band checksum (int64 sum of the fp32 bit
+        # patterns, exact) must equal the checksum of the slot rank 0 received.
+        last = outs[(args.steps - 1) % 2][: band.rows]
+        coll_dev = device if args.dist_backend == "nccl" else "cpu"
+        mine = last.view(torch.int32).to(torch.int64).sum().reshape(1).to(coll_dev)
+        sums = [torch.zeros(1, dtype=torch.int64, device=coll_dev) for _ in range(world)]
+        dist.all_gather(sums, mine)
+        if rank == 0:
+            got = [gather.frame[r, : D.band_rows(cfg.height, world, r).rows].view(torch.int32).to(torch.int64).sum()
+                   for r in range(world)]
+            gather_ok = all(int(g.item()) == int(s_.item()) for g, s_ in zip(got, sums))
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=device if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
@@ -221,7 +242,9 @@ def main():
             parity = {"parity_max_rel": max_rel, "parity_bit_exact_frac": round(exact, 6)}
         gather_note = {}
         if world > 1:
-            gather_note = {"gather": "batched isend/irecv star to rank 0 (RCCL), pipelined with the next frame"}
+            gather_note = {"gather": ("batched isend/irecv star to rank 0 (RCCL), pipelined with the next frame"
+                                      if args.dist_backend == "nccl" else "host-staged gloo gather (test mode)"),
+                           "gather_checksums_match": gather_ok}
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,

@@ -62,7 +62,7 @@ def init_from_env(backend: str) -> Tuple[int, int, int]:
         os.environ.setdefault("MASTER_PORT", "29517")
         kwargs = {}
         if backend == "nccl":
-            kwargs["device_id"] = torch.device("cuda", local)
+            kwargs["device_id"] = torch.device("cuda", local)  # one GPU per rank (RCCL)
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
     return rank, world, local
 
@@ -82,6 +82,10 @@ class BandGather:
         self.frame: Optional[torch.Tensor] = None
         if band.rank == 0:
             self.frame = torch.empty((band.world, band.rows_max, width, 4), dtype=dtype, device=device)
+        # gloo cannot move device tensors point to point: stage through host memory (tests only;
+        # the benchmark's multi-GPU path is RCCL).
+        self.host_staged = (band.world > 1 and torch.device(device).type == "cuda"
+                            and dist.get_backend(group) == "gloo")
 
     def start(self, band_out: torch.Tensor):
         """Post the gather of ``band_out`` ((rows_max, W, 4)); returns the list of work handles."""
@@ -89,12 +93,28 @@ class BandGather:
         if b.world == 1:
             self.frame[0].copy_(band_out)
             return []
+        if self.host_staged:
+            self._gather_host_staged(band_out)
+            return []
         if b.rank == 0:
             self.frame[0].copy_(band_out)
             ops = [dist.P2POp(dist.irecv, self.frame[r], r, self.group) for r in range(1, b.world)]
         else:
             ops = [dist.P2POp(dist.isend, band_out, 0, self.group)]
         return dist.batch_isend_irecv(ops)
+
+    def _gather_host_staged(self, band_out: torch.Tensor) -> None:
+        b = self.band
+        if b.rank == 0:
+            self.frame[0].copy_(band_out)
+            bufs = [torch.empty(tuple(band_out.shape), dtype=band_out.dtype) for _ in range(1, b.world)]
+            works = [dist.irecv(buf, r, self.group) for r, buf in zip(range(1, b.world), bufs)]
+            for w in works:
+                w.wait()
+            for r, buf in zip(range(1, b.world), bufs):
+                self.frame[r].copy_(buf)
+        else:
+            dist.send(band_out.cpu(), 0, self.group)
 
     @staticmethod
     def wait(handles) -> None:
