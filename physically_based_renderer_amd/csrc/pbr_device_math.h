@@ -8,6 +8,7 @@
 // invariants out of the light loop, which compute the identical values once instead of per light.
 #pragma once
 #include <hip/hip_runtime.h>
+#include "libm_f32.h"
 
 namespace pbr {
 
@@ -76,16 +77,49 @@ __device__ __forceinline__ float sqrt_nr(float x) {
 __device__ __forceinline__ bool in_win(float x, float lo, float hi) { return fabsf(x) >= lo && fabsf(x) <= hi; }
 __device__ __forceinline__ bool zero_or_in(float x, float lo, float hi) { return x == 0.0f || in_win(x, lo, hi); }
 
-// pow(x, 5.0) of FresnelSchlick (LightingUtil.hlsl:46) for x = 1 - saturate(.) in [0, 1]:
-// x^2 is exact in fp64 and x^5 carries at most 2^-52 relative error before the one rounding to
-// fp32, which made it correctly rounded on every float in [0, 1] we checked (glibc's powf is not:
-// 0.07% of its results are 1 ulp off). Five fp64/convert ops instead of ocml's ~40-op powf.
-__device__ __forceinline__ float pow5(float x) {
-    double d = (double)x;
-    double d2 = d * d;
-    double d4 = d2 * d2;
-    return (float)(d4 * d);
+// pow(x, 5.0) of FresnelSchlick (LightingUtil.hlsl:46) for x = 1 - saturate(.) in {0} U [2^-24, 1].
+//
+// The oracle computes glibc's powf, which is 1 ulp off the correctly rounded x^5 on 0.06% of
+// inputs. Where that matters is kD = 1 - F: with p = x^5, one ulp of p becomes p / (1 - p) ulps of kD.
+//  * pow5_glibc: glibc's algorithm bit for bit (libm_f32.h). Used for the IBL ambient's Fresnel
+//    (Default.hlsl:141-146; once per pixel, and there kD scales the whole term), and by pow5_light
+//    on the grazing band.
+//  * pow5_light: per light, fp64 x^5 (2^-52 relative before the one rounding to fp32; correctly
+//    rounded on every float in [0, 1] checked) while x <= 0.99, glibc's algorithm above. On the fp64
+//    side p <= 0.951, so a 1-ulp difference from glibc moves that light's diffuse term by at most
+//    19.4 ulp (1.2e-6 relative) and leaves every other term exact -- 8x inside the 1e-5 parity bar
+//    even for a pixel lit by that light alone. x > 0.99 needs H.V < 0.01 and is rare per wave.
+// The tables are read from LDS (PBR_POW5_LDS, filled by load_libm_tables at kernel entry) or from
+// constant memory.
+#ifndef PBR_POW5_LDS
+#define PBR_POW5_LDS 1
+#endif
+#if PBR_POW5_LDS
+__shared__ pbr_powf_log2_entry g_lds_powf_log2[16];
+__shared__ uint64_t g_lds_exp2f[32];
+// Every work-item of the block calls this, and a barrier follows before the first pow5.
+__device__ __forceinline__ void load_libm_tables() {
+    const int t = threadIdx.x;
+    if (t < 16) g_lds_powf_log2[t] = pbr_powf_log2_tab[t];
+    if (t >= 32 && t < 64) g_lds_exp2f[t - 32] = pbr_exp2f_tab[t - 32];
 }
+#define PBR_POW5_TABLES g_lds_powf_log2, g_lds_exp2f
+#else
+__device__ __forceinline__ void load_libm_tables() {}
+#define PBR_POW5_TABLES pbr_powf_log2_tab, pbr_exp2f_tab
+#endif
+#ifndef PBR_POW5_GLIBC_FROM  // x above which pow5_light switches to glibc's algorithm
+#define PBR_POW5_GLIBC_FROM 0.99f
+#endif
+__device__ __forceinline__ float pow5_glibc(float x) { return pbr_pow5_unit(x, PBR_POW5_TABLES); }
+__device__ __forceinline__ float pow5_light(float x) {
+    if (__builtin_expect(x > PBR_POW5_GLIBC_FROM, 0)) return pow5_glibc(x);
+    const double d = (double)x;
+    const double d2 = d * d;
+    return (float)(d2 * d2 * d);
+}
+// powf for the spot cone and the gamma encode: glibc's algorithm (libm_f32.h), all special cases.
+__device__ __forceinline__ float powf_glibc(float x, float y) { return pbr_powf(x, y); }
 
 constexpr float kPi = 3.14159265359f;  // LightingUtil.hlsl:59, 103 (an fp32 literal in HLSL)
 constexpr float kInvGamma = 1.0f / 2.2f;  // Default.hlsl:155
@@ -192,7 +226,7 @@ __device__ __forceinline__ f3 brdf_cook_torrance(const PixelInvariants& q, f3 ra
     float g = ggx_l * q.ggx_v;
     // FresnelSchlick(H, V, F0)
     float cos_theta = hsat(dot3(h, q.v));
-    float p = pow5(1.0f - cos_theta);
+    float p = pow5_light(1.0f - cos_theta);
     f3 f = mk3(q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p);
     // specular = (NDF*G)*F / (4*NdotV*NdotL + 0.001); the denominator is >= 0.001 by construction
     float ndf_g = ndf * g;
@@ -251,7 +285,7 @@ __device__ __forceinline__ bool point_or_spot_light(const PixelInvariants& q, f3
     float att = qdiv<FAST>(1.0f, qrecip<FAST>(dsat * dsat));
     if (SPOT) {
         f3 nl = mk3(-l.x, -l.y, -l.z);
-        att *= powf(hmax(dot3(nl, mk3(d.x, d.y, d.z)), 0.0f), s.w);  // :163, SpotPower in .w
+        att *= powf_glibc(hmax(dot3(nl, mk3(d.x, d.y, d.z)), 0.0f), s.w);  // :163, SpotPower in .w
     }
     out = brdf_cook_torrance<FAST>(q, mk3(s.x * att, s.y * att, s.z * att), l, h, ok);
     return true;
@@ -259,8 +293,8 @@ __device__ __forceinline__ bool point_or_spot_light(const PixelInvariants& q, f3
 
 // WorldToSkyUV (LightingUtil.hlsl:216-225); .xy only.
 __device__ __forceinline__ void world_to_sky_uv(f3 c, float& u, float& v) {
-    float ux = atan2f(c.z, c.x);
-    float uy = asinf(c.y);
+    float ux = pbr_atan2f(c.z, c.x);  // glibc's algorithms, bit for bit (libm_f32.h)
+    float uy = pbr_asinf(c.y);
     ux = ux * 0.1591f;
     uy = uy * 0.3183f;
     ux = ux + 0.5f;

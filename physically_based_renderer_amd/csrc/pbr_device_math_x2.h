@@ -4,7 +4,7 @@
 // Every operation is the scalar fast path's operation applied element-wise: a packed instruction
 // rounds each element exactly like its scalar form, so each pixel of the pair gets the bits the
 // scalar fast path (and therefore the compiler's full IEEE sequences) would give it. Transcendental
-// seeds (v_rcp_f32, v_sqrt_f32), compares, selects and the fp64 pow5 have no packed form and run
+// seeds (v_rcp_f32, v_sqrt_f32), compares, selects and the fp64 powf (pow5) have no packed form and run
 // per element. Pixels that leave the fast-path window are re-evaluated by the scalar exact path.
 #pragma once
 #include "pbr_device_math.h"
@@ -53,7 +53,7 @@ __device__ __forceinline__ v2 sqrt_nr(v2 x) {
     s = vsel(rm <= 0.0f, sm, s);
     return vsel(rp > 0.0f, sp, s);
 }
-__device__ __forceinline__ v2 pow5(v2 x) { return v2{pow5(x.x), pow5(x.y)}; }
+__device__ __forceinline__ v2 pow5_light(v2 x) { return v2{pow5_light(x.x), pow5_light(x.y)}; }
 // |x| in [lo, hi] per element (false for NaN), as an int mask (-1 / 0).
 __device__ __forceinline__ v2i in_win(v2 x, float lo, float hi) {
     v2 a = __builtin_elementwise_abs(x);
@@ -131,7 +131,7 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, const Recip2&
     v2 ggx_l = div_nr(n_dot_l, recip_nr(n_dot_l * q.one_minus_k + q.k));
     v2 g = ggx_l * q.ggx_v;
     v2 cos_theta = vsat(dot3(h, q.v));
-    v2 p = pow5(1.0f - cos_theta);
+    v2 p = pow5_light(1.0f - cos_theta);
     f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
     v2 ndf_g = ndf * g;
     v2 denom = q.four_n_dot_v * n_dot_l + 0.001f;
@@ -176,7 +176,7 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
     v2 att = div_nr(splat(1.0f), recip_nr(dsat * dsat));
     if (SPOT) {
         v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
-        att *= v2{powf(c.x, s.w), powf(c.y, s.w)};
+        att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
     return brdf_x2(q, rpi, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
 }

@@ -269,7 +269,7 @@ __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float a
         // Default.hlsl:141-146: kS = FresnelSchlick(N, V, F0); kD = (1 - kS)(1 - metallic);
         // irradiance = env.Sample(linear-wrap, WorldToSkyUV(N)); ambient = kD * (irradiance * albedo)
         const float cos_theta = hsat(dot3(p.n, q.v));
-        const float pw = pow5(1.0f - cos_theta);
+        const float pw = pow5_glibc(1.0f - cos_theta);
         const f3 ks = mk3(p.f0.x + q.one_minus_f0.x * pw, p.f0.y + q.one_minus_f0.y * pw, p.f0.z + q.one_minus_f0.z * pw);
         const f3 kd = mk3((1.0f - ks.x) * q.one_minus_metal, (1.0f - ks.y) * q.one_minus_metal,
                           (1.0f - ks.z) * q.one_minus_metal);
@@ -285,7 +285,8 @@ __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float a
     if (APPLY_AO) ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
     f3 lit = add3(ambient, direct);
     lit = mk3(lit.x / (lit.x + 1.0f), lit.y / (lit.y + 1.0f), lit.z / (lit.z + 1.0f));  // Default.hlsl:153
-    return make_float4(powf(lit.x, kInvGamma), powf(lit.y, kInvGamma), powf(lit.z, kInvGamma), ps.opacity);
+    return make_float4(powf_glibc(lit.x, kInvGamma), powf_glibc(lit.y, kInvGamma), powf_glibc(lit.z, kInvGamma),
+                       ps.opacity);
 }
 
 }  // namespace
@@ -298,6 +299,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                             unsigned long long* __restrict__ cull_stats,
                                                             bool exact_only) {
     __shared__ Lds s;
+    load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
+    __syncthreads();
 
     const int tid = threadIdx.x;
     const int xa = blockIdx.x * kTileW + 2 * (tid & 31);
@@ -442,6 +445,8 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
                                                              unsigned long long* __restrict__ cull_stats,
                                                              bool exact_only) {
     __shared__ Lds s;
+    load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
+    __syncthreads();
     const int tid = threadIdx.x;
     const int x = blockIdx.x * kTileW1 + (tid & (kTileW1 - 1));
     const int y = blockIdx.y * kTileH + (tid / kTileW1);

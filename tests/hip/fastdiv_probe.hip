@@ -1,5 +1,5 @@
 // tests/hip/fastdiv_probe.hip -- TEST-ONLY probe of the exact fast division building blocks on gfx950.
-// Built and run by tests/test_gpu_fastdiv.py. Counts disagreements with the compiler's correctly
+// Built and run by tests/test_gpu_probes.py. Counts disagreements with the compiler's correctly
 // rounded IEEE division (built with -fhip-fp32-correctly-rounded-divide-sqrt).
 #include <hip/hip_runtime.h>
 #include <cstdint>

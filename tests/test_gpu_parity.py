@@ -1,8 +1,9 @@
 """GPU parity: the gfx950 kernel (through the C ABI) against the CPU oracle and the golden vectors.
 
 Tolerance (north_star): |gpu - cpu| <= 1e-5 * |cpu| per RGBA channel, fp32, NaN == NaN. The kernel
-uses the oracle's operation order, no FMA contraction and correctly rounded div/sqrt, so most
-channels are bit-identical; the residue comes from device powf/atan2f/asinf (ocml) vs glibc.
+uses the oracle's operation order, no FMA contraction and correctly rounded div/sqrt, and evaluates
+the sky UV's atan2f/asinf with glibc's own algorithms (csrc/libm_f32.h), so most channels are
+bit-identical; the residue comes from device powf (ocml) vs glibc in the gamma encode and spot cone.
 Culled vs unculled and band vs full-frame comparisons are required to be bit-identical.
 """
 import os
@@ -254,3 +255,32 @@ def test_fast_path_is_bit_identical_to_exact_only(seed, shading_ctx, gpu, env_ma
                 e = O.rel_err(fast[finite], ref[finite])
                 print(f"adversarial seed {seed}: max_rel (finite) {e.max():.3g}, "
                       f"nan-pattern agreement {np.mean(np.isnan(fast) == np.isnan(ref)):.6f}")
+
+
+def test_ibl_near_poles_and_seam(shading_ctx, gpu, env_map):
+    """WorldToSkyUV (LightingUtil.hlsl:216-225) is ill-conditioned at the poles (asin' -> inf as
+    |N.y| -> 1) and at the atan2 seam (N.z -> 0, N.x < 0): a one-ulp libm difference there moves the
+    texel coordinate by up to 1.6e-4 relative. With csrc/libm_f32.h the sampled UVs must be the
+    oracle's bit for bit, so every channel must agree far inside the tolerance."""
+    rng = np.random.default_rng(77)
+    h, w = 64, 512
+    n_px = h * w
+    eps = (np.sign(rng.uniform(-1, 1, (2, n_px))) * 10.0 ** rng.uniform(-7, -1, (2, n_px)))
+    pole = np.stack([eps[0], np.where(rng.uniform(size=n_px) < 0.5, 1.0, -1.0), eps[1]])
+    seam = np.stack([-rng.uniform(0.05, 1, n_px), rng.uniform(-1, 1, n_px), eps[1]])
+    rand = rng.normal(size=(3, n_px))
+    pick = rng.integers(0, 3, n_px)
+    n = np.where(pick == 0, pole, np.where(pick == 1, seam, rand))
+    n = (n / np.linalg.norm(n, axis=0)).astype(np.float32)
+    n[:, :64] = np.array([[0.0, 1.0, 0.0], [0.0, -1.0, 0.0], [-1.0, 0.0, 0.0], [-1.0, 0.0, -0.0]] * 16,
+                         np.float32).T  # exact poles and the seam itself, both signs of zero
+    p = np.zeros((15, h, w), np.float32)
+    p[0:3] = rng.uniform(-5, 5, (3, h, w))
+    p[3:6] = n.reshape(3, h, w)
+    p[6:15] = rng.uniform(0, 1, (9, h, w))
+    for flags in (0, N.PBR_FLAG_APPLY_AO):
+        pc = PassConstants(ambient_mode=N.PBR_AMBIENT_IBL_DIFFUSE, flags=flags, eye_pos_w=(0.0, 0.0, -10.0))
+        got = gpu_shade(shading_ctx, p, pc, env_map, gpu)
+        ref = O.shade(list(p), oracle_pass_from_constants(pc), None, env_map, n_threads=8)
+        e = report(f"IBL poles/seam flags={flags}", got, ref)
+        assert e.max() <= 1e-6  # only the gamma powf (<= 1 ulp) may differ

@@ -1,0 +1,72 @@
+"""Device-level proofs behind the kernel's exactness claims ("exact fast path"):
+
+* fastdiv_probe.hip -- v_rcp_f32 + one Newton step is RN(1/b) for every b with exponent in
+  [-64, 64] (the window the fast path admits), and the Markstein quotient equals IEEE a / b on
+  random operands inside the window;
+* libm_probe.hip -- the device build of libm_f32.h (WorldToSkyUV's atan2f / asinf) returns the host
+  glibc's bits: asinf on every float in [-1, 1], atanf on every finite float, and 2^27 random
+  atan2f pairs.
+
+Both are compiled here with the product's fp flags (csrc/Makefile FPFLAGS).
+"""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FLAGS = ["-O3", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result", "-fPIC", "-shared", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "-I", os.path.join(ROOT, "physically_based_renderer_amd", "csrc")]
+
+
+@pytest.fixture(scope="module")
+def probes(tmp_path_factory, gpu):
+    d = tmp_path_factory.mktemp("probes")
+    libs = {}
+    for name in ("fastdiv_probe", "libm_probe"):
+        so = str(d / f"{name}.so")
+        subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, os.path.join(ROOT, "tests", "hip", f"{name}.hip"), "-o", so,
+                        "-lpthread"], check=True)
+        libs[name] = ctypes.CDLL(so)
+    return libs
+
+
+def test_reciprocal_is_correctly_rounded_in_window(probes):
+    L = probes["fastdiv_probe"]
+    bad, first = ctypes.c_ulonglong(), ctypes.c_uint()
+    assert L.probe_recip(-64, 64, ctypes.byref(bad), ctypes.byref(first)) == 0
+    assert bad.value == 0, hex(first.value)
+
+
+@pytest.mark.parametrize("alo,ahi,blo,bhi", [(-96, 60, -60, 60), (-30, 30, -30, 30), (-5, 5, -5, 5)])
+def test_markstein_quotient_is_ieee(probes, alo, ahi, blo, bhi):
+    L = probes["fastdiv_probe"]
+    bad, bad_r, ex = ctypes.c_ulonglong(), ctypes.c_ulonglong(), (ctypes.c_float * 2)()
+    assert L.probe_div(ctypes.c_ulonglong(777 + alo), 65536, 16, alo, ahi, blo, bhi, ctypes.byref(bad),
+                       ctypes.byref(bad_r), ex) == 0
+    assert bad.value == 0 and bad_r.value == 0, (ex[0], ex[1])
+
+
+@pytest.mark.parametrize("which,ranges", [(0, [(0, 0x3F800000), (0x80000000, 0xBF800000)]),
+                                          (1, [(0, 0x7F7FFFFF), (0x80000000, 0xFF7FFFFF)])])
+def test_device_libm_port_equals_glibc(probes, which, ranges):
+    L = probes["libm_probe"]
+    L.probe_unary.restype = ctypes.c_longlong
+    L.probe_unary.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    for lo, hi in ranges:
+        first = ctypes.c_uint32()
+        bad = L.probe_unary(which, lo, hi, ctypes.byref(first))
+        assert bad == 0, f"{['asinf', 'atan2f(y,1)'][which]}: {bad} mismatches, first 0x{first.value:08x}"
+
+
+def test_device_atan2f_pairs_equal_glibc(probes):
+    L = probes["libm_probe"]
+    L.probe_atan2_pairs.restype = ctypes.c_longlong
+    L.probe_atan2_pairs.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_float),
+                                    ctypes.POINTER(ctypes.c_float)]
+    y, x = ctypes.c_float(), ctypes.c_float()
+    bad = L.probe_atan2_pairs(2024, 1 << 27, ctypes.byref(y), ctypes.byref(x))
+    assert bad == 0, f"{bad} mismatches, first atan2f({y.value!r}, {x.value!r})"

@@ -133,3 +133,20 @@ def test_band_partition_covers_rows_once(height, world):
             assert b.row_begin % 8 == 0 and b.row_end % 8 == 0
     if height == 8192 and world == 8:
         assert all(b.rows == 1024 for b in bands)
+
+
+def test_sky_uv_libm_port_matches_host_glibc(tmp_path):
+    """libm_f32.h (the kernel's atan2f/asinf for WorldToSkyUV, LightingUtil.hlsl:216-225) restated on
+    the host must equal glibc bit for bit; tools/libm_port_check.c without --quick is the exhaustive
+    version of this check, tests/test_gpu_probes.py the device one."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "lpc")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fno-builtin", "-I",
+                    os.path.join(root, "physically_based_renderer_amd", "csrc"),
+                    os.path.join(root, "tools", "libm_port_check.c"), "-o", exe, "-lm", "-lpthread"], check=True)
+    out = subprocess.run([exe, "--quick"], check=True, capture_output=True, text=True).stdout
+    print(out)
+    assert out.count("mismatches 0") == 7, out
