@@ -2,8 +2,9 @@
 
 Tolerance (north_star): |gpu - cpu| <= 1e-5 * |cpu| per RGBA channel, fp32, NaN == NaN. The kernel
 uses the oracle's operation order, no FMA contraction and correctly rounded div/sqrt, and evaluates
-the sky UV's atan2f/asinf with glibc's own algorithms (csrc/libm_f32.h), so most channels are
-bit-identical; the residue comes from device powf (ocml) vs glibc in the gamma encode and spot cone.
+atan2f/asinf/powf with glibc's own algorithms (csrc/libm_f32.h), so nearly all channels are
+bit-identical; the residue comes from the per-light pow(x, 5) off the grazing band, where the kernel
+uses a correctly rounded fp64 x^5 instead of glibc's powf (pbr_device_math.h, pow5_light: <= 1.2e-6).
 Culled vs unculled and band vs full-frame comparisons are required to be bit-identical.
 """
 import os
@@ -260,8 +261,9 @@ def test_fast_path_is_bit_identical_to_exact_only(seed, shading_ctx, gpu, env_ma
 def test_ibl_near_poles_and_seam(shading_ctx, gpu, env_map):
     """WorldToSkyUV (LightingUtil.hlsl:216-225) is ill-conditioned at the poles (asin' -> inf as
     |N.y| -> 1) and at the atan2 seam (N.z -> 0, N.x < 0): a one-ulp libm difference there moves the
-    texel coordinate by up to 1.6e-4 relative. With csrc/libm_f32.h the sampled UVs must be the
-    oracle's bit for bit, so every channel must agree far inside the tolerance."""
+    texel coordinate by up to 1.6e-4 relative, and at grazing N.V the Fresnel kD = 1 - F cancels
+    (one ulp of pow(x, 5) -> up to 1e-4). With no lights every transcendental on this path is glibc's
+    algorithm (csrc/libm_f32.h), so the frame must be the oracle's bit for bit."""
     rng = np.random.default_rng(77)
     h, w = 64, 512
     n_px = h * w
@@ -282,5 +284,5 @@ def test_ibl_near_poles_and_seam(shading_ctx, gpu, env_map):
         pc = PassConstants(ambient_mode=N.PBR_AMBIENT_IBL_DIFFUSE, flags=flags, eye_pos_w=(0.0, 0.0, -10.0))
         got = gpu_shade(shading_ctx, p, pc, env_map, gpu)
         ref = O.shade(list(p), oracle_pass_from_constants(pc), None, env_map, n_threads=8)
-        e = report(f"IBL poles/seam flags={flags}", got, ref)
-        assert e.max() <= 1e-6  # only the gamma powf (<= 1 ulp) may differ
+        report(f"IBL poles/seam flags={flags}", got, ref)
+        assert O.bit_equal(got, ref).all()

@@ -135,10 +135,11 @@ def test_band_partition_covers_rows_once(height, world):
         assert all(b.rows == 1024 for b in bands)
 
 
-def test_sky_uv_libm_port_matches_host_glibc(tmp_path):
-    """libm_f32.h (the kernel's atan2f/asinf for WorldToSkyUV, LightingUtil.hlsl:216-225) restated on
-    the host must equal glibc bit for bit; tools/libm_port_check.c without --quick is the exhaustive
-    version of this check, tests/test_gpu_probes.py the device one."""
+def test_libm_port_matches_host_glibc(tmp_path):
+    """libm_f32.h (the kernel's atan2f/asinf for WorldToSkyUV, LightingUtil.hlsl:216-225, and powf for
+    Fresnel, spot cone and gamma) restated on the host must equal glibc bit for bit (this also pins
+    the host: the oracle's powf is glibc's x86-64 FMA variant). tools/libm_port_check.c without
+    --quick is the exhaustive version of this check, tests/test_gpu_probes.py the device one."""
     import os
     import subprocess
 

@@ -1,0 +1,72 @@
+"""Turn tools/profile_round.sh output (gpurun_out/prof_<tag>) into the committed evidence:
+profiles/<tag>/{kernel_stats,pmc_*}.csv and the per-workload entry of profiles/pmc_summary.json
+that bench.py reads for roofline.traffic.
+
+HBM bytes per launch = FETCH_SIZE x 2 + WRITE_SIZE (KiB; gfx950 FETCH_SIZE reports half of a
+coalesced read, MI355X_MICROARCH.md "HBM"), averaged over the shading kernel's dispatches.
+usage: python tools/pmc_summarize.py <tag> <workload> <pixels> <bytes_per_px> <lights> <revision>
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def find(pattern):
+    hits = sorted(glob.glob(pattern, recursive=True))
+    if not hits:
+        raise SystemExit(f"missing {pattern}")
+    return hits[0]
+
+
+def per_kernel(path, kernel="shade_tile"):
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel not in row.get("Kernel_Name", row.get("Name", "")):
+                continue
+            vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main():
+    tag, workload, pixels, bpp, lights, revision = sys.argv[1:7]
+    pixels, bpp, lights = int(pixels), int(bpp), int(lights)
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(find(f"{src}/kt/**/*kernel_stats.csv"), os.path.join(dst, f"kernel_stats_{workload}.csv"))
+    shutil.copy(os.path.join(src, "kt.log"), os.path.join(dst, f"bench_{workload}.log"))
+    counters = {}
+    for name in ("fetch", "write", "sq", "busy"):
+        p = find(f"{src}/pmc_{name}/**/*counter_collection.csv")
+        shutil.copy(p, os.path.join(dst, f"pmc_{name}_{workload}.csv"))
+        counters.update(per_kernel(p))
+    hbm = counters["FETCH_SIZE"] * 2 * 1024 + counters["WRITE_SIZE"] * 1024
+    alg = pixels * bpp
+    entry = {
+        "hbm_bytes_per_launch": hbm,
+        "fetch_size_kib": counters["FETCH_SIZE"],
+        "write_size_kib": counters["WRITE_SIZE"],
+        "correction": "FETCH_SIZE x2 (gfx950 reports half of a coalesced read: MI355X_MICROARCH.md HBM); "
+                      "WRITE_SIZE as reported; KiB",
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": hbm / alg,
+        "sq": {k: v for k, v in sorted(counters.items()) if k.startswith(("SQ_", "GRBM_"))},
+        "valu_insts_per_pixel_light": counters["SQ_INSTS_VALU"] * 64 / pixels / max(lights, 1),
+        "source": f"profiles/{tag}/pmc_*_{workload}.csv (rocprofv3 --pmc, separate passes, bench.py --steps 5)",
+        "kernel_revision": revision,
+    }
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    summary = json.load(open(path)) if os.path.exists(path) else {}
+    summary[workload] = entry
+    json.dump(summary, open(path, "w"), indent=1)
+    print(json.dumps(entry, indent=1))
+
+
+if __name__ == "__main__":
+    main()
