@@ -13,6 +13,7 @@ import os
 import shutil
 import sys
 
+N_SIMD = 256 * 4  # MI355X: 256 CUs x 4 SIMDs
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -58,6 +59,9 @@ def main():
         "traffic_over_algorithmic": hbm / alg,
         "sq": {k: v for k, v in sorted(counters.items()) if k.startswith(("SQ_", "GRBM_"))},
         "valu_insts_per_pixel_light": counters["SQ_INSTS_VALU"] * 64 / pixels / max(lights, 1),
+        # SQ_ACTIVE_INST_VALU counts quad-cycles summed over waves; GRBM_GUI_ACTIVE is summed over the 8
+        # XCDs (MI355X_MICROARCH.md): VALU-issue cycles per SIMD over kernel cycles.
+        "valu_issue_busy": counters["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / (counters["GRBM_GUI_ACTIVE"] / 8),
         "source": f"profiles/{tag}/pmc_*_{workload}.csv (rocprofv3 --pmc, separate passes, bench.py --steps 5)",
         "kernel_revision": revision,
     }
