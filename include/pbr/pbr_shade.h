@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBR_ABI_VERSION 1
+#define PBR_ABI_VERSION 2
 #define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
 
 typedef enum pbr_status {
@@ -121,6 +121,44 @@ int pbr_set_env_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int
 int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rgba, int64_t out_row_stride,
                       void* stream);
 
+/* ---- Frame composition: sky pass, output format, HDR textures (ABI 2) -------------------------- */
+
+/* Output pixel formats. RGBA32F is what pbr_shade_gbuffer writes. RGBA8_UNORM is the reference's
+ * back buffer (DXGI_FORMAT_R8G8B8A8_UNORM, d3dApp.h:124; presented by PBRApp::Draw, PBRApp.cpp:274-279),
+ * converted with the D3D FLOAT -> UNORM rule: NaN -> 0, clamp to [0, 1], c * 255 + 0.5, truncate. */
+typedef enum pbr_output_format {
+    PBR_OUTPUT_RGBA32F = 0,
+    PBR_OUTPUT_RGBA8_UNORM = 1
+} pbr_output_format;
+
+typedef struct pbr_frame_desc {
+    void* out;                   /* DEVICE: RGBA32F 16 B/px (16-byte aligned) or RGBA8 4 B/px (4-byte aligned) */
+    int64_t out_row_stride;      /* pixels between output rows, >= width */
+    int32_t format;              /* pbr_output_format */
+    int32_t pad0;
+    /* Optional DEVICE coverage plane, one byte per pixel, `coverage_row_stride` bytes per row:
+     * nonzero = geometry (shaded by PS, Default.hlsl:47-161); 0 = background, which gets the sky pass
+     * of Skybox.hlsl:37-49 instead (the reference draws the sky dome where no geometry wrote depth,
+     * PBRApp.cpp:319-320, 856-875). For a background pixel the G-buffer normal planes hold the sky
+     * sample direction (the sky dome's interpolated local position, Skybox.hlsl:24); its other planes
+     * are not used. NULL = every pixel is geometry. */
+    const uint8_t* coverage;
+    int64_t coverage_row_stride;
+} pbr_frame_desc;
+
+/* The sky texture g_SkyArray[0] (PBRApp.cpp:1200-1204, sampled by Skybox.hlsl:45 with g_SamLinearWrap):
+ * R16G16B16A16_UNORM, HOST texels as pbr_set_env_map. Required when a frame has background pixels. */
+int pbr_set_sky_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int32_t height, void* stream);
+
+/* fp32 RGBA variants of pbr_set_env_map / pbr_set_sky_map (HOST width*height*4 floats, e.g. a decoded
+ * RGBE .hdr environment, Assets/<set>/<set>_Env.hdr): the texels are used as given, no UNORM decode. */
+int pbr_set_env_map_f32(pbr_context* ctx, const float* texels, int32_t width, int32_t height, void* stream);
+int pbr_set_sky_map_f32(pbr_context* ctx, const float* texels, int32_t width, int32_t height, void* stream);
+
+/* pbr_shade_gbuffer with the frame options above, in one pass over the G-buffer (the sky and the
+ * format conversion are fused into the shading kernel). Asynchronous on `stream`. */
+int pbr_shade_frame(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* frame, void* stream);
+
 /* Tiled-culling statistics of the last culled pass on `stream` (synchronises that stream):
  * total surviving point/spot lights summed over tiles, and the tile count. */
 int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream);
@@ -162,6 +200,13 @@ typedef struct pbr_scene_desc {
  * covered (non-background) pixels, or a negative pbr_status. */
 int64_t pbr_gbuffer_fill(const pbr_scene_desc* scene, int32_t row_begin, int32_t row_end, float* const* planes,
                          int64_t row_stride, int32_t n_threads);
+
+/* pbr_gbuffer_fill that also writes the coverage plane pbr_shade_frame consumes: one byte per pixel,
+ * 1 = geometry, 0 = background (config 1's sky around the sphere; the other scenes are fully covered).
+ * Background pixels get the view direction in their normal planes (the sky dome point they see). */
+int64_t pbr_gbuffer_fill_coverage(const pbr_scene_desc* scene, int32_t row_begin, int32_t row_end,
+                                  float* const* planes, int64_t row_stride, uint8_t* coverage,
+                                  int64_t coverage_stride, int32_t n_threads);
 
 /* The light list and pass constants of a benchmark scene (`n_lights` point lights; kind 1 uses one
  * light at (20, 20, -20), strength 100, PBRApp.cpp:490-491). `pass->lights` is set to `lights`. */

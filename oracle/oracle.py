@@ -154,6 +154,111 @@ def rel_err(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     return np.where(same_inf, 0.0, e)
 
 
+class _Frame(ctypes.Structure):
+    _fields_ = [
+        ("env_rgba", ctypes.c_void_p),
+        ("env_w", ctypes.c_int32),
+        ("env_h", ctypes.c_int32),
+        ("sky_rgba", ctypes.c_void_p),
+        ("sky_w", ctypes.c_int32),
+        ("sky_h", ctypes.c_int32),
+        ("coverage", ctypes.c_void_p),
+        ("coverage_stride", ctypes.c_int64),
+        ("format", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
+    ]
+
+
+OUTPUT_RGBA32F = 0
+OUTPUT_RGBA8 = 1
+
+
+def decode_unorm16(texels: np.ndarray) -> np.ndarray:
+    """R16G16B16A16_UNORM -> RGBA fp32 exactly as the C oracle does ((float)u / 65535.0f)."""
+    lib = ctypes.CDLL(ORACLE_SO)
+    src = np.ascontiguousarray(texels, dtype=np.uint16)
+    dst = np.empty(src.shape, np.float32)
+    lib.oracle_decode_unorm16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    lib.oracle_decode_unorm16(src.ctypes.data, src.size, dst.ctypes.data)
+    return dst
+
+
+def _texture(t):
+    """An RGBA texture for the frame entry: uint16 UNORM (decoded here) or float32, (h, w, 4)."""
+    if t is None:
+        return None
+    a = np.asarray(t)
+    if a.dtype == np.uint16:
+        a = decode_unorm16(a)
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    assert a.ndim == 3 and a.shape[2] == 4
+    return a
+
+
+def _shade_frame(fn, planes, opass: OraclePass, lights, env, sky, coverage, fmt, n_threads):
+    assert len(planes) == NUM_PLANES
+    ref_plane = next(p for p in planes if p is not None)
+    h, w = ref_plane.shape
+    keep = []
+    ptrs = (ctypes.c_void_p * NUM_PLANES)()
+    for i, p in enumerate(planes):
+        if p is None:
+            ptrs[i] = None
+            continue
+        a = np.ascontiguousarray(p, dtype=np.float32)
+        assert a.shape == (h, w)
+        keep.append(a)
+        ptrs[i] = a.ctypes.data
+    n_lights = opass.n_dir + opass.n_point + opass.n_spot
+    lights_arr = np.ascontiguousarray(lights, dtype=np.float32).reshape(-1, 12) if n_lights else np.zeros((1, 12), np.float32)
+    fr = _Frame()
+    env_a, sky_a = _texture(env), _texture(sky)
+    keep += [env_a, sky_a]
+    if env_a is not None:
+        fr.env_rgba, fr.env_h, fr.env_w = env_a.ctypes.data, env_a.shape[0], env_a.shape[1]
+    if sky_a is not None:
+        fr.sky_rgba, fr.sky_h, fr.sky_w = sky_a.ctypes.data, sky_a.shape[0], sky_a.shape[1]
+    if coverage is not None:
+        cov = np.ascontiguousarray(coverage, dtype=np.uint8)
+        assert cov.shape == (h, w)
+        keep.append(cov)
+        fr.coverage, fr.coverage_stride = cov.ctypes.data, w
+    fr.format = int(fmt)
+    out = np.empty((h, w, 4), np.uint8 if fmt == OUTPUT_RGBA8 else np.float32)
+    cp = opass.to_c()
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),
+                   ctypes.POINTER(_Pass), ctypes.c_void_p, ctypes.POINTER(_Frame), ctypes.c_void_p, ctypes.c_int64,
+                   ctypes.c_int]
+    rc = fn(w, h, w, ptrs, ctypes.byref(cp), lights_arr.ctypes.data, ctypes.byref(fr), out.ctypes.data, w,
+            int(n_threads))
+    if rc != 0:
+        raise ValueError(f"oracle rejected arguments (rc={rc})")
+    return out
+
+
+def shade_frame(planes, opass: OraclePass, lights=None, env=None, sky=None, coverage=None, fmt=OUTPUT_RGBA32F,
+                n_threads: int = 1) -> np.ndarray:
+    """PS + the sky pass on background pixels (coverage == 0), RGBA fp32 or RGBA8 (pbr_oracle.c)."""
+    return _shade_frame(ctypes.CDLL(ORACLE_SO).oracle_shade_frame, planes, opass, lights, env, sky, coverage, fmt,
+                        n_threads)
+
+
+def shade_frame_ref(planes, opass: OraclePass, lights=None, env=None, sky=None, coverage=None,
+                    fmt=OUTPUT_RGBA32F) -> np.ndarray:
+    """The same through the reference's own LightingUtil.hlsl (oracle/_ref); this container only."""
+    return _shade_frame(ctypes.CDLL(REF_SO).ref_shade_frame, planes, opass, lights, env, sky, coverage, fmt, 1)
+
+
+def unorm8(c: np.ndarray) -> np.ndarray:
+    """D3D FLOAT -> UNORM8 of the C oracle, element-wise (oracle_unorm8)."""
+    lib = ctypes.CDLL(ORACLE_SO)
+    lib.oracle_unorm8.restype = ctypes.c_uint8
+    lib.oracle_unorm8.argtypes = [ctypes.c_float]
+    flat = np.asarray(c, np.float32).ravel()
+    return np.array([lib.oracle_unorm8(float(v)) for v in flat], np.uint8).reshape(np.shape(c))
+
+
 def bit_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Elementwise bit equality, treating any NaN as equal to any NaN."""
     a = np.asarray(a, np.float32)

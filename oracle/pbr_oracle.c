@@ -157,18 +157,19 @@ static inline void world_to_sky_uv(v3 c, float* u, float* v) {
     *v = uy;
 }
 
-/* Linear-wrap bilinear sample of an R16G16B16A16_UNORM texture (g_SamLinearWrap,
- * PBRApp.cpp:1157-1162). Texel value = u16 / 65535 (UNORM decode). */
+/* Linear-wrap bilinear sample (g_SamLinearWrap, PBRApp.cpp:1157-1162) of an RGBA fp32 texture: an
+ * R16G16B16A16_UNORM texture is decoded once to u16 / 65535 (oracle_decode_unorm16); an HDR texture
+ * is used as given. */
 static inline int wrap_index(float f, int n) {
     if (!(f == f) || f > 2.0e9f || f < -2.0e9f) return 0; /* NaN coordinate: weights are NaN anyway */
     int i = (int)f % n;
     return i < 0 ? i + n : i;
 }
-static inline float texel(const uint16_t* env, int w, int x, int y, int c) {
-    return (float)env[((size_t)y * (size_t)w + (size_t)x) * 4u + (size_t)c] / 65535.0f;
+static inline float texel(const float* env, int w, int x, int y, int c) {
+    return env[((size_t)y * (size_t)w + (size_t)x) * 4u + (size_t)c];
 }
 static inline float lerpf_h(float a, float b, float t) { return a + t * (b - a); }
-static v3 sample_linear_wrap(const uint16_t* env, int w, int h, float u, float v) {
+static v3 sample_linear_wrap(const float* env, int w, int h, float u, float v) {
     float x = u * (float)w - 0.5f;
     float y = v * (float)h - 0.5f;
     float x0f = floorf(x), y0f = floorf(y);
@@ -191,9 +192,14 @@ typedef struct {
     const float* const* planes;
     const oracle_pass* pass;
     const oracle_light* lights;
-    const uint16_t* env;
+    const float* env;
     int env_w, env_h;
-    float* out;
+    const float* sky;
+    int sky_w, sky_h;
+    const uint8_t* coverage;
+    int64_t coverage_stride;
+    int format;
+    void* out_any;
 } job_t;
 
 /* PS, Default.hlsl:47-161, one pixel. N is the already-resolved G-buffer normal (lines 50, 104-109
@@ -268,25 +274,71 @@ static void shade_pixel(const job_t* j, int64_t idx, float* o) {
     o[3] = ps->opacity; /* Default.hlsl:160 */
 }
 
+/* The sky pass for a background pixel, Skybox.hlsl:37-49: sampleCoord = normalize(PosW) (the sky
+ * dome's interpolated local position, here the G-buffer normal planes), WorldToSkyUV, sample
+ * g_SkyArray[0] with linear-wrap, Reinhard, gamma, alpha 1. */
+static void sky_pixel(const job_t* j, int64_t idx, float* o) {
+    const float* const* P = j->planes;
+    v3 c = norm3(v3make(P[ORACLE_NX][idx], P[ORACLE_NY][idx], P[ORACLE_NZ][idx]));
+    float su, sv;
+    world_to_sky_uv(c, &su, &sv);
+    v3 col = sample_linear_wrap(j->sky, j->sky_w, j->sky_h, su, sv);
+    col = v3make(col.x / (col.x + 1.0f), col.y / (col.y + 1.0f), col.z / (col.z + 1.0f));
+    const float inv_gamma = 1.0f / 2.2f;
+    o[0] = powf(col.x, inv_gamma);
+    o[1] = powf(col.y, inv_gamma);
+    o[2] = powf(col.z, inv_gamma);
+    o[3] = 1.0f;
+}
+
+/* D3D FLOAT -> UNORM8 (the R8G8B8A8_UNORM back buffer, d3dApp.h:124; D3D11 functional spec
+ * "FLOAT -> UNORM"): NaN -> 0; clamp to [0, 1]; c * 255 + 0.5 in fp32; truncate. */
+uint8_t oracle_unorm8(float c) {
+    if (!(c == c)) return 0;
+    c = c > 1.0f ? 1.0f : c;
+    c = c < 0.0f ? 0.0f : c;
+    return (uint8_t)(c * 255.0f + 0.5f);
+}
+
 static void* run_rows(void* arg) {
     const job_t* j = (const job_t*)arg;
     for (int y = j->row0; y < j->row1; ++y) {
         for (int x = 0; x < j->width; ++x) {
-            shade_pixel(j, (int64_t)y * j->stride + x, j->out + ((int64_t)y * j->out_stride + x) * 4);
+            const int64_t idx = (int64_t)y * j->stride + x;
+            const int64_t off = (int64_t)y * j->out_stride + x;
+            float px[4];
+            if (j->coverage && j->coverage[(int64_t)y * j->coverage_stride + x] == 0)
+                sky_pixel(j, idx, px);
+            else
+                shade_pixel(j, idx, px);
+            if (j->format == ORACLE_OUTPUT_RGBA8) {
+                uint8_t* o8 = (uint8_t*)j->out_any + off * 4;
+                for (int c = 0; c < 4; ++c) o8[c] = oracle_unorm8(px[c]);
+            } else {
+                float* o = (float*)j->out_any + off * 4;
+                for (int c = 0; c < 4; ++c) o[c] = px[c];
+            }
         }
     }
     return NULL;
 }
 
-int oracle_shade(int width, int height, int64_t stride, const float* const* planes,
-                 const oracle_pass* pass, const oracle_light* lights,
-                 const uint16_t* env_rgba16, int env_w, int env_h,
-                 float* out, int64_t out_stride, int n_threads) {
-    if (width < 0 || height < 0 || !planes || !pass || !out) return -1;
+void oracle_decode_unorm16(const uint16_t* src, int64_t n_values, float* dst) {
+    for (int64_t i = 0; i < n_values; ++i) dst[i] = (float)src[i] / 65535.0f; /* R16G16B16A16_UNORM */
+}
+
+int oracle_shade_frame(int width, int height, int64_t stride, const float* const* planes, const oracle_pass* pass,
+                       const oracle_light* lights, const oracle_frame* frame, void* out, int64_t out_stride,
+                       int n_threads) {
+    if (width < 0 || height < 0 || !planes || !pass || !frame || !out) return -1;
     if (stride < width || out_stride < width) return -1;
+    if (frame->format != ORACLE_OUTPUT_RGBA32F && frame->format != ORACLE_OUTPUT_RGBA8) return -1;
     if (pass->n_dir < 0 || pass->n_point < 0 || pass->n_spot < 0) return -1;
     if (pass->n_dir + pass->n_point + pass->n_spot > 0 && !lights) return -1;
-    if (pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE && (!env_rgba16 || env_w <= 0 || env_h <= 0)) return -1;
+    if (pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE &&
+        (!frame->env_rgba || frame->env_w <= 0 || frame->env_h <= 0)) return -1;
+    if (frame->coverage && (!frame->sky_rgba || frame->sky_w <= 0 || frame->sky_h <= 0 ||
+                            frame->coverage_stride < width)) return -1;
     for (int p = 0; p < ORACLE_AO; ++p)
         if (!planes[p]) return -1;
     if (pass->apply_ao && !planes[ORACLE_AO]) return -1;
@@ -308,10 +360,16 @@ int oracle_shade(int width, int height, int64_t stride, const float* const* plan
         j->planes = planes;
         j->pass = pass;
         j->lights = lights;
-        j->env = env_rgba16;
-        j->env_w = env_w;
-        j->env_h = env_h;
-        j->out = out;
+        j->env = frame->env_rgba;
+        j->env_w = frame->env_w;
+        j->env_h = frame->env_h;
+        j->sky = frame->sky_rgba;
+        j->sky_w = frame->sky_w;
+        j->sky_h = frame->sky_h;
+        j->coverage = frame->coverage;
+        j->coverage_stride = frame->coverage_stride;
+        j->format = frame->format;
+        j->out_any = out;
     }
     if (n_threads == 1) {
         run_rows(&jobs[0]);
@@ -326,4 +384,27 @@ int oracle_shade(int width, int height, int64_t stride, const float* const* plan
     run_rows(&jobs[0]);
     for (int t = 1; t <= started; ++t) pthread_join(th[t], NULL);
     return 0;
+}
+
+int oracle_shade(int width, int height, int64_t stride, const float* const* planes,
+                 const oracle_pass* pass, const oracle_light* lights,
+                 const uint16_t* env_rgba16, int env_w, int env_h,
+                 float* out, int64_t out_stride, int n_threads) {
+    if (pass && pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE && (!env_rgba16 || env_w <= 0 || env_h <= 0))
+        return -1;
+    oracle_frame fr = {0};
+    float* env = NULL;
+    if (env_rgba16 && env_w > 0 && env_h > 0) {
+        const int64_t n = (int64_t)env_w * env_h * 4;
+        env = (float*)malloc(sizeof(float) * (size_t)n);
+        if (!env) return -2;
+        oracle_decode_unorm16(env_rgba16, n, env);
+        fr.env_rgba = env;
+        fr.env_w = env_w;
+        fr.env_h = env_h;
+    }
+    fr.format = ORACLE_OUTPUT_RGBA32F;
+    const int rc = oracle_shade_frame(width, height, stride, planes, pass, lights, &fr, out, out_stride, n_threads);
+    free(env);
+    return rc;
 }

@@ -70,6 +70,32 @@ int oracle_shade(int width, int height, int64_t stride, const float* const* plan
                  const uint16_t* env_rgba16, int env_w, int env_h,
                  float* out, int64_t out_stride, int n_threads);
 
+/* ---- Frame composition (product: pbr_shade_frame) --------------------------------------------- */
+
+enum { ORACLE_OUTPUT_RGBA32F = 0, ORACLE_OUTPUT_RGBA8 = 1 };
+
+typedef struct oracle_frame {
+    const float* env_rgba;    /* IBL texture as RGBA fp32 (decode UNORM16 with oracle_decode_unorm16) */
+    int32_t env_w, env_h;
+    const float* sky_rgba;    /* sky texture g_SkyArray[0] (Skybox.hlsl:45), RGBA fp32 */
+    int32_t sky_w, sky_h;
+    const uint8_t* coverage;  /* NULL = all geometry; else 0 = background -> Skybox.hlsl PS */
+    int64_t coverage_stride;  /* bytes */
+    int32_t format;           /* ORACLE_OUTPUT_*: RGBA fp32 (16 B/px) or RGBA8 UNORM (4 B/px) */
+    int32_t pad0;
+} oracle_frame;
+
+/* As oracle_shade, with the sky pass on background pixels and the output format of `frame`. */
+int oracle_shade_frame(int width, int height, int64_t stride, const float* const* planes,
+                       const oracle_pass* pass, const oracle_light* lights, const oracle_frame* frame,
+                       void* out, int64_t out_stride, int n_threads);
+
+/* R16G16B16A16_UNORM decode: dst[i] = (float)src[i] / 65535.0f. */
+void oracle_decode_unorm16(const uint16_t* src, int64_t n_values, float* dst);
+
+/* D3D FLOAT -> UNORM8: NaN -> 0, clamp [0, 1], c * 255 + 0.5 (fp32), truncate. */
+uint8_t oracle_unorm8(float c);
+
 #ifdef __cplusplus
 }
 #endif

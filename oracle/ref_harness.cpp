@@ -65,13 +65,15 @@ namespace ref_mix {
 struct Texture2D {
     const uint16_t* texels;
     int w, h;
+    const float* ftexels = nullptr;  // RGBA fp32 texture (HDR, or UNORM16 pre-decoded), used if set
     static int wrap(float f, int n) {
         if (!(f == f) || f > 2.0e9f || f < -2.0e9f) return 0;
         int i = (int)f % n;
         return i < 0 ? i + n : i;
     }
     float fetch(int x, int y, int c) const {
-        return (float)texels[((size_t)y * (size_t)w + (size_t)x) * 4u + (size_t)c] / 65535.0f;
+        const size_t i = ((size_t)y * (size_t)w + (size_t)x) * 4u + (size_t)c;
+        return ftexels ? ftexels[i] : (float)texels[i] / 65535.0f;
     }
     float3 Sample(float3 uvw) const {  // only .xy is a coordinate (Default.hlsl:144)
         float x = uvw.x * (float)w - 0.5f, y = uvw.y * (float)h - 0.5f;
@@ -153,60 +155,110 @@ float3 direct_light(const oracle_pass& ps, const oracle_light* lights, const ref
 
 }  // namespace
 
+namespace {
+
+// PS (Default.hlsl:47-161) for one G-buffer pixel.
+float4 ps_pixel(const float* const* planes, int64_t i, const oracle_pass& ps, const oracle_light* lights,
+                const Texture2D& env) {
+    float3 PosW(planes[ORACLE_PX][i], planes[ORACLE_PY][i], planes[ORACLE_PZ][i]);
+    float3 N(planes[ORACLE_NX][i], planes[ORACLE_NY][i], planes[ORACLE_NZ][i]);
+    float3 g_CameraPosW(ps.eye[0], ps.eye[1], ps.eye[2]);
+    // Default.hlsl:53
+    float3 V = normalize(g_CameraPosW - PosW);
+    float3 diffuseAlbedo(planes[ORACLE_AR][i], planes[ORACLE_AG][i], planes[ORACLE_AB][i]);
+    float metallic = planes[ORACLE_METAL][i];
+    float roughness = planes[ORACLE_ROUGH][i];
+    float3 F0;
+    if (ps.use_f0_plane) {  // Default.hlsl:92
+        F0 = float3(planes[ORACLE_F0R][i], planes[ORACLE_F0G][i], planes[ORACLE_F0B][i]);
+    } else {  // Default.hlsl:94-95
+        F0 = float3(ps.fresnel_r0[0], ps.fresnel_r0[1], ps.fresnel_r0[2]);
+        F0 = lerp(F0, diffuseAlbedo, metallic);
+    }
+    // Default.hlsl:121-133 (only the first four members are read by the BRDF)
+    ref_d4::Material mat = {diffuseAlbedo, metallic, F0, roughness, float3(1.0f), ps.opacity,
+                            float3(0.0f), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    // Default.hlsl:135-137
+    float3 directLight = direct_light(ps, lights, mat, PosW, N, V);
+    float3 ambient;
+    if (ps.ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE) {
+        // Default.hlsl:141-146 (the commented-out IBL block)
+        float3 kS = ref_d4::FresnelSchlick(N, V, F0);
+        float3 kD = 1.0f - kS;
+        kD *= (1.0f - metallic);
+        float3 irradiance = env.Sample(ref_d4::WorldToSkyUV(N));
+        float3 diffuse = irradiance * diffuseAlbedo;
+        ambient = (kD * diffuse);
+    } else {
+        // Default.hlsl:150  g_AmbientLight * diffuseAlbedo
+        float4 g_AmbientLight{ps.ambient[0], ps.ambient[1], ps.ambient[2], 1.0f};
+        ambient = g_AmbientLight.rgb() * diffuseAlbedo;
+    }
+    if (ps.apply_ao) ambient = ambient * planes[ORACLE_AO][i];  // extension, off in the reference
+    float3 litColor = ambient + directLight;
+    // Default.hlsl:153, 155
+    litColor = litColor / (litColor + float3(1.0f, 1.0f, 1.0f));
+    litColor = pow(litColor, (1.0f / 2.2f));
+    return float4{litColor.x, litColor.y, litColor.z, ps.opacity};  // Default.hlsl:160
+}
+
+// Skybox.hlsl:41-49 (PS) for one background pixel; PosW = the G-buffer normal planes.
+float4 sky_pixel(const float* const* planes, int64_t i, const Texture2D& sky) {
+    float3 PosW(planes[ORACLE_NX][i], planes[ORACLE_NY][i], planes[ORACLE_NZ][i]);
+    float3 sampleCoord = normalize(PosW);
+    sampleCoord = ref_d4::WorldToSkyUV(sampleCoord);
+    float3 skyColor = sky.Sample(sampleCoord);
+    skyColor = skyColor / (skyColor + float3(1.0f, 1.0f, 1.0f));
+    skyColor = pow(skyColor, (1.0f / 2.2f));
+    return float4{skyColor.x, skyColor.y, skyColor.z, 1.0f};
+}
+
+uint8_t unorm8(float c) {  // D3D FLOAT -> UNORM (the R8G8B8A8_UNORM back buffer, d3dApp.h:124)
+    if (!(c == c)) return 0;
+    c = c > 1.0f ? 1.0f : c;
+    c = c < 0.0f ? 0.0f : c;
+    return (uint8_t)(c * 255.0f + 0.5f);
+}
+
+}  // namespace
+
+extern "C" int ref_shade_frame(int width, int height, int64_t stride, const float* const* planes,
+                               const oracle_pass* pass, const oracle_light* lights, const oracle_frame* frame,
+                               void* out, int64_t out_stride, int /*n_threads*/) {
+    if (!planes || !pass || !frame || !out || width < 0 || height < 0) return -1;
+    if (pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE && !frame->env_rgba) return -1;
+    if (frame->coverage && !frame->sky_rgba) return -1;
+    Texture2D env{nullptr, frame->env_w, frame->env_h, frame->env_rgba};
+    Texture2D sky{nullptr, frame->sky_w, frame->sky_h, frame->sky_rgba};
+    for (int y = 0; y < height; ++y) {
+        for (int x = 0; x < width; ++x) {
+            const int64_t i = (int64_t)y * stride + x;
+            const bool background = frame->coverage && frame->coverage[(int64_t)y * frame->coverage_stride + x] == 0;
+            const float4 c = background ? sky_pixel(planes, i, sky) : ps_pixel(planes, i, *pass, lights, env);
+            const int64_t off = ((int64_t)y * out_stride + x) * 4;
+            if (frame->format == ORACLE_OUTPUT_RGBA8) {
+                uint8_t* o = static_cast<uint8_t*>(out) + off;
+                o[0] = unorm8(c.x); o[1] = unorm8(c.y); o[2] = unorm8(c.z); o[3] = unorm8(c.w);
+            } else {
+                float* o = static_cast<float*>(out) + off;
+                o[0] = c.x; o[1] = c.y; o[2] = c.z; o[3] = c.w;
+            }
+        }
+    }
+    return 0;
+}
+
 extern "C" int ref_shade(int width, int height, int64_t stride, const float* const* planes, const oracle_pass* pass,
                          const oracle_light* lights, const uint16_t* env_rgba16, int env_w, int env_h, float* out,
                          int64_t out_stride, int /*n_threads*/) {
     if (!planes || !pass || !out || width < 0 || height < 0) return -1;
     if (pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE && !env_rgba16) return -1;
-    const oracle_pass& ps = *pass;
     Texture2D env{env_rgba16, env_w, env_h};
     for (int y = 0; y < height; ++y) {
         for (int x = 0; x < width; ++x) {
-            const int64_t i = (int64_t)y * stride + x;
-            float3 PosW(planes[ORACLE_PX][i], planes[ORACLE_PY][i], planes[ORACLE_PZ][i]);
-            float3 N(planes[ORACLE_NX][i], planes[ORACLE_NY][i], planes[ORACLE_NZ][i]);
-            float3 g_CameraPosW(ps.eye[0], ps.eye[1], ps.eye[2]);
-            // Default.hlsl:53
-            float3 V = normalize(g_CameraPosW - PosW);
-            float3 diffuseAlbedo(planes[ORACLE_AR][i], planes[ORACLE_AG][i], planes[ORACLE_AB][i]);
-            float metallic = planes[ORACLE_METAL][i];
-            float roughness = planes[ORACLE_ROUGH][i];
-            float3 F0;
-            if (ps.use_f0_plane) {  // Default.hlsl:92
-                F0 = float3(planes[ORACLE_F0R][i], planes[ORACLE_F0G][i], planes[ORACLE_F0B][i]);
-            } else {  // Default.hlsl:94-95
-                F0 = float3(ps.fresnel_r0[0], ps.fresnel_r0[1], ps.fresnel_r0[2]);
-                F0 = lerp(F0, diffuseAlbedo, metallic);
-            }
-            // Default.hlsl:121-133 (only the first four members are read by the BRDF)
-            ref_d4::Material mat = {diffuseAlbedo, metallic, F0, roughness, float3(1.0f), ps.opacity,
-                                    float3(0.0f), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-            // Default.hlsl:135-137
-            float3 directLight = direct_light(ps, lights, mat, PosW, N, V);
-            float3 ambient;
-            if (ps.ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE) {
-                // Default.hlsl:141-146 (the commented-out IBL block)
-                float3 kS = ref_d4::FresnelSchlick(N, V, F0);
-                float3 kD = 1.0f - kS;
-                kD *= (1.0f - metallic);
-                float3 irradiance = env.Sample(ref_d4::WorldToSkyUV(N));
-                float3 diffuse = irradiance * diffuseAlbedo;
-                ambient = (kD * diffuse);
-            } else {
-                // Default.hlsl:150  g_AmbientLight * diffuseAlbedo
-                float4 g_AmbientLight{ps.ambient[0], ps.ambient[1], ps.ambient[2], 1.0f};
-                ambient = g_AmbientLight.rgb() * diffuseAlbedo;
-            }
-            if (ps.apply_ao) ambient = ambient * planes[ORACLE_AO][i];  // extension, off in the reference
-            float3 litColor = ambient + directLight;
-            // Default.hlsl:153, 155
-            litColor = litColor / (litColor + float3(1.0f, 1.0f, 1.0f));
-            litColor = pow(litColor, (1.0f / 2.2f));
+            const float4 c = ps_pixel(planes, (int64_t)y * stride + x, *pass, lights, env);
             float* o = out + ((int64_t)y * out_stride + x) * 4;
-            o[0] = litColor.x;
-            o[1] = litColor.y;
-            o[2] = litColor.z;
-            o[3] = ps.opacity;  // Default.hlsl:160
+            o[0] = c.x; o[1] = c.y; o[2] = c.z; o[3] = c.w;
         }
     }
     return 0;

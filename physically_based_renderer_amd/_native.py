@@ -23,6 +23,8 @@ PBR_FLAG_F0_PLANE = 1 << 0
 PBR_FLAG_APPLY_AO = 1 << 1
 PBR_FLAG_TILED_CULLING = 1 << 2
 PBR_FLAG_EXACT_ONLY = 1 << 3
+PBR_OUTPUT_RGBA32F = 0
+PBR_OUTPUT_RGBA8_UNORM = 1
 PBR_SCENE_SPHERE_RUSTEDIRON = 1
 PBR_SCENE_RANDOM_COVERED = 2
 PBR_SCENE_PLANE_MATERIALS = 4
@@ -83,6 +85,17 @@ class GBufferSoA(ctypes.Structure):
     ]
 
 
+class FrameDesc(ctypes.Structure):
+    _fields_ = [
+        ("out", ctypes.c_void_p),
+        ("out_row_stride", ctypes.c_int64),
+        ("format", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
+        ("coverage", ctypes.c_void_p),
+        ("coverage_row_stride", ctypes.c_int64),
+    ]
+
+
 class SceneAssets(ctypes.Structure):
     _fields_ = [
         ("rust_metallic", ctypes.c_void_p),
@@ -118,10 +131,21 @@ SIGNATURES = {
                                        ctypes.c_void_p]),
     "pbr_shade_gbuffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GBufferSoA), ctypes.c_void_p,
                                          ctypes.c_int64, ctypes.c_void_p]),
+    "pbr_set_env_map_f32": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_void_p]),
+    "pbr_set_sky_map": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_void_p]),
+    "pbr_set_sky_map_f32": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_void_p]),
+    "pbr_shade_frame": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GBufferSoA), ctypes.POINTER(FrameDesc),
+                                       ctypes.c_void_p]),
     "pbr_last_cull_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "pbr_gbuffer_fill": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,
                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int32]),
+    "pbr_gbuffer_fill_coverage": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,
+                                                   ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_void_p,
+                                                   ctypes.c_int64, ctypes.c_int32]),
     "pbr_scene_pass": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.POINTER(Light),
                                       ctypes.POINTER(PassDesc)]),
     "pbr_strerror": (ctypes.c_char_p, [ctypes.c_int]),

@@ -37,7 +37,12 @@ constexpr uint64_t kLightStream = 0x4C49474854535452ull;  // independent stream 
 
 struct Row {
     float* p[15];
+    uint8_t* cov;  // coverage row (1 = geometry, 0 = background), or nullptr
 };
+
+inline void set_cov(Row r, int x, bool geometry) {
+    if (r.cov) r.cov[x] = geometry ? 1 : 0;
+}
 
 void fill_random_covered(const pbr_scene_desc& sc, int y, Row r) {
     const pbr_scene_assets* as = sc.assets;
@@ -92,6 +97,7 @@ int64_t fill_sphere(const pbr_scene_desc& sc, int y, Row r) {
         dx *= il, dy *= il, dz *= il;
         const double oz = -5.0;  // eye (0, 0, -5)
         const double b = oz * dz, c = oz * oz - 1.0, disc = b * b - c;
+        set_cov(r, x, disc >= 0.0);
         if (disc >= 0.0) {
             ++covered;
             const double tt = -b - std::sqrt(disc);
@@ -114,13 +120,15 @@ int64_t fill_sphere(const pbr_scene_desc& sc, int y, Row r) {
             r.p[kRough][x] = (float)as->rust_roughness[ti] / 255.0f;
             r.p[kF0r][x] = r.p[kF0g][x] = r.p[kF0b][x] = lerp_h(0.04f, 0.5f, metal);
         } else {
-            // Background: a far point on the view ray, black and rough (the sky pass is out of scope).
+            // Background: a far point on the view ray, black and rough; the normal planes carry the
+            // view direction, i.e. the point of the camera-centred sky dome this pixel sees (the sky
+            // pass samples it, Skybox.hlsl:22-24, 41).
             r.p[kPosX][x] = (float)(dx * 100.0);
             r.p[kPosY][x] = (float)(dy * 100.0);
             r.p[kPosZ][x] = (float)(oz + dz * 100.0);
-            r.p[kNx][x] = (float)-dx;
-            r.p[kNy][x] = (float)-dy;
-            r.p[kNz][x] = (float)-dz;
+            r.p[kNx][x] = (float)dx;
+            r.p[kNy][x] = (float)dy;
+            r.p[kNz][x] = (float)dz;
             r.p[kAr][x] = r.p[kAg][x] = r.p[kAb][x] = 0.0f;
             r.p[kMetal][x] = 0.0f;
             r.p[kRough][x] = 1.0f;
@@ -183,6 +191,13 @@ bool assets_ok(const pbr_scene_desc* sc) {
 
 extern "C" int64_t pbr_gbuffer_fill(const pbr_scene_desc* scene, int32_t row_begin, int32_t row_end,
                                     float* const* planes, int64_t row_stride, int32_t n_threads) {
+    return pbr_gbuffer_fill_coverage(scene, row_begin, row_end, planes, row_stride, nullptr, 0, n_threads);
+}
+
+extern "C" int64_t pbr_gbuffer_fill_coverage(const pbr_scene_desc* scene, int32_t row_begin, int32_t row_end,
+                                             float* const* planes, int64_t row_stride, uint8_t* coverage,
+                                             int64_t coverage_stride, int32_t n_threads) {
+    if (coverage && scene && coverage_stride < scene->width) return PBR_ERR_INVALID_ARGUMENT;
     if (!scene || !planes || scene->width <= 0 || scene->height <= 0) return PBR_ERR_INVALID_ARGUMENT;
     if (row_begin < 0 || row_end < row_begin || row_end > scene->height || row_stride < scene->width)
         return PBR_ERR_INVALID_ARGUMENT;
@@ -200,11 +215,13 @@ extern "C" int64_t pbr_gbuffer_fill(const pbr_scene_desc* scene, int32_t row_beg
         for (int y = r0; y < r1; ++y) {
             Row r;
             for (int i = 0; i < 15; ++i) r.p[i] = planes[i] + (int64_t)(y - row_begin) * row_stride;
+            r.cov = coverage ? coverage + (int64_t)(y - row_begin) * coverage_stride : nullptr;
             switch (scene->kind) {
                 case PBR_SCENE_SPHERE_RUSTEDIRON: covered[t] += fill_sphere(*scene, y, r); break;
                 case PBR_SCENE_RANDOM_COVERED: fill_random_covered(*scene, y, r); covered[t] += scene->width; break;
                 default: fill_plane(*scene, y, r); covered[t] += scene->width; break;
             }
+            if (r.cov && scene->kind != PBR_SCENE_SPHERE_RUSTEDIRON) std::memset(r.cov, 1, (size_t)scene->width);
         }
     };
     std::vector<std::thread> th;

@@ -23,10 +23,14 @@ struct pbr_context {
     hipEvent_t ring_done[kRing] = {};
     bool ring_used[kRing] = {};
     int ring_next = 0;
-    // Environment: u16 upload buffer and the decoded fp32 RGBA texture.
-    uint16_t* d_env_u16 = nullptr;
-    float4* d_env = nullptr;
-    int env_w = 0, env_h = 0, env_capacity = 0;
+    // Textures: the environment (IBL, g_SkyArray[1]) and the sky (g_SkyArray[0]), each kept as fp32
+    // RGBA on the device (decoded once from R16G16B16A16_UNORM, or uploaded as fp32).
+    struct Texture {
+        uint16_t* d_u16 = nullptr;  // UNORM16 upload staging
+        float4* d = nullptr;
+        int w = 0, h = 0, capacity = 0;
+    };
+    Texture env, sky;
     // Current pass.
     pbr::PassArgs pass{};
     int ambient_mode = 0;
@@ -123,8 +127,10 @@ int pbr_context_destroy(pbr_context* ctx) {
             if (ctx->h_ring[i]) (void)hipHostFree(ctx->h_ring[i]);
         }
         if (ctx->d_lights) (void)hipFree(ctx->d_lights);
-        if (ctx->d_env_u16) (void)hipFree(ctx->d_env_u16);
-        if (ctx->d_env) (void)hipFree(ctx->d_env);
+        for (pbr_context::Texture* t : {&ctx->env, &ctx->sky}) {
+            if (t->d_u16) (void)hipFree(t->d_u16);
+            if (t->d) (void)hipFree(t->d);
+        }
         if (ctx->d_cull_stats) (void)hipFree(ctx->d_cull_stats);
     }
     delete ctx;
@@ -192,7 +198,14 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
     return PBR_OK;
 }
 
-int pbr_set_env_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int32_t height, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// Upload a width x height RGBA texture (UNORM16 -> decoded on the device, or fp32 as given) into slot
+// `t`. Synchronous with respect to the host buffer: it may be released on return.
+int set_texture(pbr_context* ctx, pbr_context::Texture& t, const void* texels, bool unorm16, int32_t width,
+                int32_t height, void* stream, const char* what) {
     if (!ctx || !texels || width <= 0 || height <= 0) return PBR_ERR_INVALID_ARGUMENT;
     if ((long long)width * height > (1ll << 26)) return PBR_ERR_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -201,39 +214,48 @@ int pbr_set_env_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int n = width * height;
     hipError_t e;
-    if (n > ctx->env_capacity) {
+    if (n > t.capacity) {
+        // Growing: the old texture may still be read by queued kernels on any stream.
         e = hipDeviceSynchronize();
-        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_env_map sync");
-        if (ctx->d_env_u16) (void)hipFree(ctx->d_env_u16);
-        if (ctx->d_env) (void)hipFree(ctx->d_env);
-        ctx->d_env_u16 = nullptr;
-        ctx->d_env = nullptr;
-        ctx->env_capacity = 0;
-        e = hipMalloc(&ctx->d_env_u16, sizeof(uint16_t) * 4 * (size_t)n);
-        if (e == hipSuccess) e = hipMalloc(&ctx->d_env, sizeof(float4) * (size_t)n);
-        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_env_map hipMalloc");
-        ctx->env_capacity = n;
+        if (e != hipSuccess) return fail_hip(ctx, e, what);
+        if (t.d_u16) (void)hipFree(t.d_u16);
+        if (t.d) (void)hipFree(t.d);
+        t.d_u16 = nullptr;
+        t.d = nullptr;
+        t.capacity = 0;
+        e = hipMalloc(&t.d_u16, sizeof(uint16_t) * 4 * (size_t)n);
+        if (e == hipSuccess) e = hipMalloc(&t.d, sizeof(float4) * (size_t)n);
+        if (e != hipSuccess) return fail_hip(ctx, e, what);
+        t.capacity = n;
     }
-    e = hipMemcpyAsync(ctx->d_env_u16, texels, sizeof(uint16_t) * 4 * (size_t)n, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_env_map copy");
-    e = pbr::launch_decode_env(ctx->d_env_u16, ctx->d_env, n, s);
-    if (e != hipSuccess) return fail_hip(ctx, e, "decode_env_kernel", PBR_ERR_LAUNCH);
-    // The host texels may be released on return: wait for the (pageable) copy to finish.
-    e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_env_map sync");
-    ctx->env_w = width;
-    ctx->env_h = height;
+    if (unorm16) {
+        e = hipMemcpyAsync(t.d_u16, texels, sizeof(uint16_t) * 4 * (size_t)n, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return fail_hip(ctx, e, what);
+        e = pbr::launch_decode_unorm16(t.d_u16, t.d, n, s);
+        if (e != hipSuccess) return fail_hip(ctx, e, "decode_unorm16_kernel", PBR_ERR_LAUNCH);
+    } else {
+        e = hipMemcpyAsync(t.d, texels, sizeof(float4) * (size_t)n, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return fail_hip(ctx, e, what);
+    }
+    e = hipStreamSynchronize(s);  // the (pageable) host texels may be released on return
+    if (e != hipSuccess) return fail_hip(ctx, e, what);
+    t.w = width;
+    t.h = height;
     return PBR_OK;
 }
 
-int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rgba, int64_t out_row_stride,
-                      void* stream) {
-    if (!ctx || !gb) return PBR_ERR_INVALID_ARGUMENT;
-    if (gb->width < 0 || gb->height < 0 || gb->row_stride < gb->width || out_row_stride < gb->width)
+bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr, void* stream) {
+    if (!ctx || !gb || !fr) return PBR_ERR_INVALID_ARGUMENT;
+    if (gb->width < 0 || gb->height < 0 || gb->row_stride < gb->width || fr->out_row_stride < gb->width)
         return PBR_ERR_INVALID_ARGUMENT;
+    if (fr->format != PBR_OUTPUT_RGBA32F && fr->format != PBR_OUTPUT_RGBA8_UNORM) return PBR_ERR_INVALID_ARGUMENT;
+    if (fr->coverage && fr->coverage_row_stride < gb->width) return PBR_ERR_INVALID_ARGUMENT;
     if (!ctx->pass_set) return PBR_ERR_NOT_READY;
     if (gb->width == 0 || gb->height == 0) return PBR_OK;  // empty frame: nothing is read or written
-    if (!out_rgba) return PBR_ERR_INVALID_ARGUMENT;
+    if (!fr->out) return PBR_ERR_INVALID_ARGUMENT;
+    if (!aligned(fr->out, fr->format == PBR_OUTPUT_RGBA8_UNORM ? 4 : 16)) return PBR_ERR_INVALID_ARGUMENT;
     const bool f0_plane = (ctx->flags & PBR_FLAG_F0_PLANE) != 0;
     const bool apply_ao = (ctx->flags & PBR_FLAG_APPLY_AO) != 0;
     const bool cull = (ctx->flags & PBR_FLAG_TILED_CULLING) != 0;
@@ -242,7 +264,8 @@ int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rg
     if (!gb->metallic || !gb->roughness) return PBR_ERR_INVALID_ARGUMENT;
     if (apply_ao && !gb->ao) return PBR_ERR_INVALID_ARGUMENT;
     if (f0_plane && (!gb->f0[0] || !gb->f0[1] || !gb->f0[2])) return PBR_ERR_INVALID_ARGUMENT;
-    if (ctx->ambient_mode == PBR_AMBIENT_IBL_DIFFUSE && !ctx->d_env) return PBR_ERR_NOT_READY;
+    if (ctx->ambient_mode == PBR_AMBIENT_IBL_DIFFUSE && !ctx->env.d) return PBR_ERR_NOT_READY;
+    if (fr->coverage && !ctx->sky.d) return PBR_ERR_NOT_READY;  // background pixels need the sky map
 
     pbr::LaunchArgs a{};
     const float* planes[15] = {gb->pos_w[0], gb->pos_w[1], gb->pos_w[2], gb->normal_w[0], gb->normal_w[1],
@@ -254,14 +277,20 @@ int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rg
     a.gb.row_stride = gb->row_stride;
     a.gb.pairs_aligned = (gb->row_stride % 2) == 0;
     for (int i = 0; i < 15; ++i)
-        if ((reinterpret_cast<uintptr_t>(a.gb.plane[i]) & 7u) != 0) a.gb.pairs_aligned = false;
+        if (!aligned(a.gb.plane[i], 8)) a.gb.pairs_aligned = false;
     a.ps = ctx->pass;
-    a.ps.env_w = ctx->env_w;
-    a.ps.env_h = ctx->env_h;
+    a.ps.env_w = ctx->env.w;
+    a.ps.env_h = ctx->env.h;
+    a.ps.sky_w = ctx->sky.w;
+    a.ps.sky_h = ctx->sky.h;
     a.lights = ctx->d_lights;
-    a.env = ctx->d_env;
-    a.out = reinterpret_cast<float4*>(out_rgba);
-    a.out_stride = out_row_stride;
+    a.env = ctx->env.d;
+    a.frame.out = fr->out;
+    a.frame.out_stride = fr->out_row_stride;
+    a.frame.format = fr->format == PBR_OUTPUT_RGBA8_UNORM ? pbr::kOutRgba8 : pbr::kOutRgba32f;
+    a.frame.coverage = fr->coverage;
+    a.frame.coverage_stride = fr->coverage_row_stride;
+    a.frame.sky = ctx->sky.d;
     a.cull_stats = ctx->d_cull_stats;
     a.ambient_mode = ctx->ambient_mode;
     a.f0_plane = f0_plane;
@@ -269,7 +298,6 @@ int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rg
     a.cull = cull;
     a.exact_only = (ctx->flags & PBR_FLAG_EXACT_ONLY) != 0;
     a.pixels_per_thread = ctx->pixels_per_thread;
-    if ((reinterpret_cast<uintptr_t>(out_rgba) & 15u) != 0) return PBR_ERR_INVALID_ARGUMENT;  // float4 stores
 
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;
@@ -282,6 +310,43 @@ int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rg
     e = pbr::launch_shade(a, s);
     if (e != hipSuccess) return fail_hip(ctx, e, "shade_tile_kernel launch", PBR_ERR_LAUNCH);
     return PBR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbr_set_env_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int32_t height, void* stream) {
+    return ctx ? set_texture(ctx, ctx->env, texels, true, width, height, stream, "pbr_set_env_map")
+               : PBR_ERR_INVALID_ARGUMENT;
+}
+
+int pbr_set_env_map_f32(pbr_context* ctx, const float* texels, int32_t width, int32_t height, void* stream) {
+    return ctx ? set_texture(ctx, ctx->env, texels, false, width, height, stream, "pbr_set_env_map_f32")
+               : PBR_ERR_INVALID_ARGUMENT;
+}
+
+int pbr_set_sky_map(pbr_context* ctx, const uint16_t* texels, int32_t width, int32_t height, void* stream) {
+    return ctx ? set_texture(ctx, ctx->sky, texels, true, width, height, stream, "pbr_set_sky_map")
+               : PBR_ERR_INVALID_ARGUMENT;
+}
+
+int pbr_set_sky_map_f32(pbr_context* ctx, const float* texels, int32_t width, int32_t height, void* stream) {
+    return ctx ? set_texture(ctx, ctx->sky, texels, false, width, height, stream, "pbr_set_sky_map_f32")
+               : PBR_ERR_INVALID_ARGUMENT;
+}
+
+int pbr_shade_gbuffer(pbr_context* ctx, const pbr_gbuffer_soa* gb, float* out_rgba, int64_t out_row_stride,
+                      void* stream) {
+    pbr_frame_desc fr{};
+    fr.out = out_rgba;
+    fr.out_row_stride = out_row_stride;
+    fr.format = PBR_OUTPUT_RGBA32F;
+    return shade(ctx, gb, &fr, stream);
+}
+
+int pbr_shade_frame(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* frame, void* stream) {
+    return shade(ctx, gb, frame, stream);
 }
 
 int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream) {

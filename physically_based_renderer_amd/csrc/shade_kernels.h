@@ -26,6 +26,20 @@ struct PassArgs {
     float opacity;
     int n_dir, n_point, n_spot;
     int env_w, env_h;
+    int sky_w, sky_h;
+};
+
+constexpr int kOutRgba32f = 0;
+constexpr int kOutRgba8 = 1;
+
+// Where and how a pass writes its pixels (pbr_frame_desc).
+struct FrameArgs {
+    void* out;                 // float4 (kOutRgba32f) or uint32 RGBA8 (kOutRgba8) per pixel
+    int64_t out_stride;        // pixels
+    int format;
+    const uint8_t* coverage;   // nullptr = every pixel is geometry; else 0 = background (sky pass)
+    int64_t coverage_stride;   // bytes
+    const float4* sky;         // sky_w * sky_h RGBA fp32 (required when coverage != nullptr)
 };
 
 struct LaunchArgs {
@@ -33,8 +47,7 @@ struct LaunchArgs {
     PassArgs ps;
     const float4* lights;  // 3 float4 per light (the reference's 48-byte Light)
     const float4* env;     // env_w * env_h RGBA fp32, or nullptr
-    float4* out;
-    int64_t out_stride;    // pixels
+    FrameArgs frame;
     unsigned long long* cull_stats;  // [sum kept lights, tiles], CULL only
     int ambient_mode;
     bool f0_plane, apply_ao, cull;
@@ -43,6 +56,6 @@ struct LaunchArgs {
 };
 
 hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);
-hipError_t launch_decode_env(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream);
+hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream);
 
 }  // namespace pbr

@@ -289,13 +289,46 @@ __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float a
                        ps.opacity);
 }
 
+// The sky pass for a background pixel (Skybox.hlsl:37-49): sampleCoord = normalize(PosW);
+// WorldToSkyUV; g_SkyArray[0].Sample(linear-wrap); Reinhard; gamma; alpha 1.
+__device__ __forceinline__ float4 sky_pixel(f3 dir, const PassArgs& ps, const float4* __restrict__ sky) {
+    const f3 c = normalize3(dir);
+    float u, v;
+    world_to_sky_uv(c, u, v);
+    f3 col = sample_linear_wrap(sky, ps.sky_w, ps.sky_h, u, v);
+    col = mk3(col.x / (col.x + 1.0f), col.y / (col.y + 1.0f), col.z / (col.z + 1.0f));
+    return make_float4(powf_glibc(col.x, kInvGamma), powf_glibc(col.y, kInvGamma), powf_glibc(col.z, kInvGamma),
+                       1.0f);
+}
+
+// D3D FLOAT -> UNORM8 (the R8G8B8A8_UNORM back buffer, d3dApp.h:124): NaN -> 0, clamp to [0, 1],
+// c * 255 + 0.5 in fp32 (no contraction), truncate.
+__device__ __forceinline__ uint32_t unorm8(float c) {
+    if (!(c == c)) return 0u;
+    c = c > 1.0f ? 1.0f : c;
+    c = c < 0.0f ? 0.0f : c;
+    return (uint32_t)(c * 255.0f + 0.5f);
+}
+
+__device__ __forceinline__ void store_pixel(const FrameArgs& fr, int64_t off, float4 c) {
+    if (fr.format == kOutRgba8) {
+        static_cast<uint32_t*>(fr.out)[off] = unorm8(c.x) | (unorm8(c.y) << 8) | (unorm8(c.z) << 16) | (unorm8(c.w) << 24);
+    } else {
+        static_cast<float4*>(fr.out)[off] = c;
+    }
+}
+
+// Coverage of a pixel: geometry unless the frame has a coverage plane holding 0 there.
+__device__ __forceinline__ bool is_geometry(const FrameArgs& fr, int x, int y) {
+    return fr.coverage == nullptr || fr.coverage[(int64_t)y * fr.coverage_stride + x] != 0;
+}
+
 }  // namespace
 
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GBufferArgs gb, PassArgs ps,
                                                             const float4* __restrict__ lights,
-                                                            const float4* __restrict__ env,
-                                                            float4* __restrict__ out, int64_t out_stride,
+                                                            const float4* __restrict__ env, FrameArgs fr,
                                                             unsigned long long* __restrict__ cull_stats,
                                                             bool exact_only) {
     __shared__ Lds s;
@@ -308,6 +341,10 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const bool va = (xa < gb.width) && (y < gb.height);
     const bool vb = (xa + 1 < gb.width) && (y < gb.height);
     const int64_t row = (int64_t)y * gb.row_stride;
+    // Geometry (PS) or background (sky pass) per pixel; background pixels take no part in the tile
+    // bounds, the exact re-pass or the lighting (a block without geometry skips it).
+    const bool ga = va && is_geometry(fr, xa, y), gb_ = vb && is_geometry(fr, xa + 1, y);
+    const bool any_geometry = fr.coverage == nullptr || __syncthreads_or(ga || gb_);
 
     const PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
                                                    vb && gb.pairs_aligned);
@@ -325,16 +362,16 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     TileBounds tb{};
     bool cull_enabled = false;
     if (CULL) {
-        const bool finite = (!va || (isfinite(pa.x) && isfinite(pa.y) && isfinite(pa.z))) &&
-                            (!vb || (isfinite(pb.x) && isfinite(pb.y) && isfinite(pb.z)));
+        const bool finite = (!ga || (isfinite(pa.x) && isfinite(pa.y) && isfinite(pa.z))) &&
+                            (!gb_ || (isfinite(pb.x) && isfinite(pb.y) && isfinite(pb.z)));
         const float big = 3.0e38f;
         float b[6];
-        b[0] = fminf(va ? pa.x : big, vb ? pb.x : big);
-        b[1] = fminf(va ? pa.y : big, vb ? pb.y : big);
-        b[2] = fminf(va ? pa.z : big, vb ? pb.z : big);
-        b[3] = fmaxf(va ? pa.x : -big, vb ? pb.x : -big);
-        b[4] = fmaxf(va ? pa.y : -big, vb ? pb.y : -big);
-        b[5] = fmaxf(va ? pa.z : -big, vb ? pb.z : -big);
+        b[0] = fminf(ga ? pa.x : big, gb_ ? pb.x : big);
+        b[1] = fminf(ga ? pa.y : big, gb_ ? pb.y : big);
+        b[2] = fminf(ga ? pa.z : big, gb_ ? pb.z : big);
+        b[3] = fmaxf(ga ? pa.x : -big, gb_ ? pb.x : -big);
+        b[4] = fmaxf(ga ? pa.y : -big, gb_ ? pb.y : -big);
+        b[5] = fmaxf(ga ? pa.z : -big, gb_ ? pb.z : -big);
 #pragma unroll
         for (int i = 0; i < 3; ++i) b[i] = wave_min(b[i]);
 #pragma unroll
@@ -360,11 +397,14 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     v2i redo = v2i{0, 0};
     const f3x2 pos2 = p.pos;
     const float ao_a = p.ao.x, ao_b = p.ao.y;
-    const f3x2 d2 = lighting_fast<CULL>(q2, pos2, v2i{ok_a ? -1 : 0, ok_b ? -1 : 0}, lights, ps, s, tb, cull_enabled,
-                                        redo, kept_total);
+    f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
+    if (any_geometry) {  // block-uniform
+        d2 = lighting_fast<CULL>(q2, pos2, v2i{ok_a ? -1 : 0, ok_b ? -1 : 0}, lights, ps, s, tb, cull_enabled, redo,
+                                 kept_total);
+    }
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
     f3 da = lane(d2, 0), db = lane(d2, 1);
-    const bool need_a = va && redo.x != 0, need_b = vb && redo.y != 0;
+    const bool need_a = ga && redo.x != 0, need_b = gb_ && redo.y != 0;
     if (__syncthreads_or(need_a || need_b)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
         f3 ea, eb;
         lighting_exact<CULL>(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, s, tb, cull_enabled,
@@ -372,14 +412,14 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         if (need_a) da = ea;
         if (need_b) db = eb;
     }
-    if (CULL && tid == 0 && cull_stats != nullptr) {
+    if (CULL && tid == 0 && cull_stats != nullptr && any_geometry) {
         atomicAdd(&cull_stats[0], (unsigned long long)kept_total);
         atomicAdd(&cull_stats[1], 1ull);
     }
 
-    float4* orow = out + (int64_t)y * out_stride;
-    if (va) orow[xa] = finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env);
-    if (vb) orow[xa + 1] = finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env);
+    const int64_t orow = (int64_t)y * fr.out_stride;
+    if (va) store_pixel(fr, orow + xa, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env) : sky_pixel(ua.n, ps, fr.sky));
+    if (vb) store_pixel(fr, orow + xa + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env) : sky_pixel(ub.n, ps, fr.sky));
 }
 
 // ---- One pixel per work-item (32x8 tiles) ---------------------------------------------------------
@@ -440,8 +480,7 @@ __device__ __forceinline__ f3 lighting_fast1(const PixelInvariants& q, f3 pos, c
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, PassArgs ps,
                                                              const float4* __restrict__ lights,
-                                                             const float4* __restrict__ env,
-                                                             float4* __restrict__ out, int64_t out_stride,
+                                                             const float4* __restrict__ env, FrameArgs fr,
                                                              unsigned long long* __restrict__ cull_stats,
                                                              bool exact_only) {
     __shared__ Lds s;
@@ -452,6 +491,8 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
     const int y = blockIdx.y * kTileH + (tid / kTileW1);
     const bool valid = (x < gb.width) && (y < gb.height);
     const int64_t idx = valid ? (int64_t)y * gb.row_stride + x : 0;  // frames are never empty here
+    const bool geom = valid && is_geometry(fr, x, y);
+    const bool any_geometry = fr.coverage == nullptr || __syncthreads_or(geom);
 
     f3 pos, n, albedo, f0;
     pos = mk3(gb.plane[0][idx], gb.plane[1][idx], gb.plane[2][idx]);
@@ -474,10 +515,10 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
     TileBounds tb{};
     bool cull_enabled = false;
     if (CULL) {
-        const bool finite = !valid || (isfinite(pos.x) && isfinite(pos.y) && isfinite(pos.z));
+        const bool finite = !geom || (isfinite(pos.x) && isfinite(pos.y) && isfinite(pos.z));
         const float big = 3.0e38f;
-        float b[6] = {valid ? pos.x : big,  valid ? pos.y : big,  valid ? pos.z : big,
-                      valid ? pos.x : -big, valid ? pos.y : -big, valid ? pos.z : -big};
+        float b[6] = {geom ? pos.x : big,  geom ? pos.y : big,  geom ? pos.z : big,
+                      geom ? pos.x : -big, geom ? pos.y : -big, geom ? pos.z : -big};
 #pragma unroll
         for (int i = 0; i < 3; ++i) b[i] = wave_min(b[i]);
 #pragma unroll
@@ -496,21 +537,24 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
 
     int kept_total = 0;
     bool redo = false;
-    f3 direct = lighting_fast1<CULL>(q, pos, lights, ps, s, tb, cull_enabled, redo, kept_total);
-    const bool need = valid && redo;
+    f3 direct = mk3(0.0f, 0.0f, 0.0f);
+    if (any_geometry) direct = lighting_fast1<CULL>(q, pos, lights, ps, s, tb, cull_enabled, redo, kept_total);
+    const bool need = geom && redo;
     if (__syncthreads_or(need)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
         f3 e, unused;
         lighting_exact<CULL>(q, q, pos, pos, need, false, lights, ps, s, tb, cull_enabled, e, unused);
         if (need) direct = e;
     }
-    if (CULL && tid == 0 && cull_stats != nullptr) {
+    if (CULL && tid == 0 && cull_stats != nullptr && any_geometry) {
         atomicAdd(&cull_stats[0], (unsigned long long)kept_total);
         atomicAdd(&cull_stats[1], 1ull);
     }
-    if (valid) out[(int64_t)y * out_stride + x] = finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env);
+    if (valid)
+        store_pixel(fr, (int64_t)y * fr.out_stride + x,
+                    geom ? finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env) : sky_pixel(q.n, ps, fr.sky));
 }
 
-__global__ void decode_env_kernel(const uint16_t* __restrict__ src, float4* __restrict__ dst, int n) {
+__global__ void decode_unorm16_kernel(const uint16_t* __restrict__ src, float4* __restrict__ dst, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
         const ushort4 t = reinterpret_cast<const ushort4*>(src)[i];
@@ -524,11 +568,11 @@ static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
     if (a.pixels_per_thread == 2) {
         dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
         hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream, a.gb,
-                           a.ps, a.lights, a.env, a.out, a.out_stride, a.cull_stats, a.exact_only);
+                           a.ps, a.lights, a.env, a.frame, a.cull_stats, a.exact_only);
     } else {
         dim3 grid((a.gb.width + kTileW1 - 1) / kTileW1, (a.gb.height + kTileH - 1) / kTileH);
         hipLaunchKernelGGL((shade_tile1_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,
-                           a.gb, a.ps, a.lights, a.env, a.out, a.out_stride, a.cull_stats, a.exact_only);
+                           a.gb, a.ps, a.lights, a.env, a.frame, a.cull_stats, a.exact_only);
     }
     return hipGetLastError();
 }
@@ -553,9 +597,9 @@ hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream) {
                                                 : dispatch_f0<kAmbientConstant>(a, stream);
 }
 
-hipError_t launch_decode_env(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream) {
+hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream) {
     if (n_texels <= 0) return hipSuccess;
-    hipLaunchKernelGGL(decode_env_kernel, dim3((n_texels + 255) / 256), dim3(256), 0, stream, src, dst, n_texels);
+    hipLaunchKernelGGL(decode_unorm16_kernel, dim3((n_texels + 255) / 256), dim3(256), 0, stream, src, dst, n_texels);
     return hipGetLastError();
 }
 

@@ -12,7 +12,9 @@ Here the same roles are:
   ``PassConstants`` + light-count defines :class:`PassConstants`
   ``UpdateMainPassCB`` / ``CopyData``     :meth:`ShadingContext.set_pass`
   sky_env SRV (t1)                        :meth:`ShadingContext.set_env_map`
+  sky_box SRV (t0) + Skybox.hlsl pass     :meth:`ShadingContext.set_sky_map`, ``coverage``
   ``DrawIndexedInstanced(PS)``            :meth:`ShadingContext.shade`
+  PS + sky dome into the R8G8B8A8 target  :meth:`ShadingContext.shade_frame`
   =====================================  ==============================================
 
 PyTorch is used only for device memory and streams. Every shading call runs the gfx950 kernel;
@@ -190,12 +192,25 @@ class ShadingContext:
                 "pbr_set_pass", self._h)
         self.pass_constants = pc
 
-    def set_env_map(self, texels: np.ndarray, stream=None) -> None:
-        t = np.ascontiguousarray(texels, dtype=np.uint16)
+    def _set_texture(self, name: str, texels: np.ndarray, stream) -> None:
+        if texels.dtype == np.uint16:
+            fn, t = name, np.ascontiguousarray(texels)
+        elif texels.dtype == np.float32:
+            fn, t = name + "_f32", np.ascontiguousarray(texels)
+        else:
+            raise ValueError(f"{name}: texels must be uint16 (R16G16B16A16_UNORM) or float32 RGBA")
         if t.ndim != 3 or t.shape[2] != 4:
-            raise ValueError("env map must be (h, w, 4) uint16")
-        N.check(self.lib.pbr_set_env_map(self._h, t.ctypes.data, t.shape[1], t.shape[0],
-                                         ctypes.c_void_p(_stream_handle(stream))), "pbr_set_env_map", self._h)
+            raise ValueError(f"{name}: texels must be (h, w, 4)")
+        N.check(getattr(self.lib, fn)(self._h, t.ctypes.data, t.shape[1], t.shape[0],
+                                      ctypes.c_void_p(_stream_handle(stream))), fn, self._h)
+
+    def set_env_map(self, texels: np.ndarray, stream=None) -> None:
+        """IBL environment (g_SkyArray[1]): (h, w, 4) uint16 UNORM or float32 (e.g. a decoded .hdr)."""
+        self._set_texture("pbr_set_env_map", texels, stream)
+
+    def set_sky_map(self, texels: np.ndarray, stream=None) -> None:
+        """Sky texture (g_SkyArray[0]) sampled for background pixels: uint16 UNORM or float32 RGBA."""
+        self._set_texture("pbr_set_sky_map", texels, stream)
 
     def shade(self, gb: GBuffer, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
         """Shade every pixel of ``gb`` into ``out`` ((H, >=W, 4) fp32 on the device), asynchronously."""
@@ -209,6 +224,39 @@ class ShadingContext:
         N.check(self.lib.pbr_shade_gbuffer(self._h, ctypes.byref(g), ctypes.c_void_p(out.data_ptr()),
                                            out.stride(0) // 4, ctypes.c_void_p(_stream_handle(stream))),
                 "pbr_shade_gbuffer", self._h)
+        return out
+
+    def shade_frame(self, gb: GBuffer, out: Optional[torch.Tensor] = None, coverage: Optional[torch.Tensor] = None,
+                    fmt: int = N.PBR_OUTPUT_RGBA32F, stream=None) -> torch.Tensor:
+        """Shade ``gb`` with the sky pass on background pixels (``coverage`` == 0; (H, >=W) uint8 on the
+        device) into ``out``: (H, W, 4) float32 for RGBA32F or (H, W, 4) uint8 for RGBA8_UNORM."""
+        dev = gb.planes.device
+        if fmt == N.PBR_OUTPUT_RGBA8_UNORM:
+            dtype, px_bytes = torch.uint8, 4
+        elif fmt == N.PBR_OUTPUT_RGBA32F:
+            dtype, px_bytes = torch.float32, 16
+        else:
+            raise ValueError("unknown output format")
+        if out is None:
+            out = torch.empty((gb.height, gb.width, 4), dtype=dtype, device=dev)
+        if out.dtype != dtype or out.dim() != 3 or out.shape[2] != 4 or out.stride(2) != 1 or out.stride(1) != 4:
+            raise ValueError("out must be (H, W, 4) with contiguous pixels of the format's dtype")
+        if out.shape[0] < gb.height or out.shape[1] < gb.width:
+            raise ValueError("out is smaller than the G-buffer")
+        f = N.FrameDesc()
+        f.out = out.data_ptr()
+        f.out_row_stride = out.stride(0) // 4
+        f.format = int(fmt)
+        if coverage is not None:
+            if coverage.dtype != torch.uint8 or coverage.dim() != 2 or coverage.stride(1) != 1:
+                raise ValueError("coverage must be a (H, W) uint8 tensor with contiguous rows")
+            if coverage.shape[0] < gb.height or coverage.shape[1] < gb.width:
+                raise ValueError("coverage is smaller than the G-buffer")
+            f.coverage = coverage.data_ptr()
+            f.coverage_row_stride = coverage.stride(0)
+        g = gb.to_c()
+        N.check(self.lib.pbr_shade_frame(self._h, ctypes.byref(g), ctypes.byref(f),
+                                         ctypes.c_void_p(_stream_handle(stream))), "pbr_shade_frame", self._h)
         return out
 
     def cull_stats(self, stream=None):

@@ -122,6 +122,27 @@ def fill_gbuffer_host(cfg: SceneConfig, row_begin: int = 0, row_end: Optional[in
     return out, int(covered)
 
 
+def fill_gbuffer_host_coverage(cfg: SceneConfig, row_begin: int = 0, row_end: Optional[int] = None,
+                               n_threads: int = 0):
+    """(planes (15, rows, width) float32, coverage (rows, width) uint8: 1 geometry / 0 background)."""
+    assets = Assets.get()
+    row_end = cfg.height if row_end is None else row_end
+    rows = row_end - row_begin
+    if rows < 0 or row_begin < 0 or row_end > cfg.height:
+        raise N.PbrError(-1, "pbr_gbuffer_fill_coverage", f"rows [{row_begin}, {row_end}) outside [0, {cfg.height})")
+    out = np.empty((N.NUM_PLANES, rows, cfg.width), np.float32)
+    cov = np.empty((rows, cfg.width), np.uint8)
+    if rows == 0:
+        return out, cov
+    ptrs = (ctypes.c_void_p * N.NUM_PLANES)(*[out[i].ctypes.data for i in range(N.NUM_PLANES)])
+    nt = n_threads or min(16, os.cpu_count() or 1)
+    d = _scene_desc(cfg, assets)
+    r = N.lib().pbr_gbuffer_fill_coverage(ctypes.byref(d), row_begin, row_end, ptrs, cfg.width, cov.ctypes.data,
+                                          cfg.width, nt)
+    N.check(int(r), "pbr_gbuffer_fill_coverage")
+    return out, cov
+
+
 def scene_pass(cfg: SceneConfig) -> PassConstants:
     """Pass constants + light list of a config (pbr_scene_pass), with its ambient mode and flags."""
     assets = Assets.get()

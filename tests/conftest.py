@@ -34,7 +34,27 @@ _ensure_built()
 
 
 def golden_names():
-    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz"))
+    """Fixtures of the PS path (oracle_shade / pbr_shade_gbuffer)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz") and not f.startswith("frame_"))
+
+
+def frame_golden_names():
+    """Fixtures of the frame path (sky pass, RGBA8 output, HDR env: pbr_shade_frame)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz") and f.startswith("frame_"))
+
+
+def load_frame_golden(name, env_png=None):
+    """dict(planes, lights, meta, expected, coverage, sky (uint16), env (uint16 / float32 / None))."""
+    z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"))  # numeric arrays only: allow_pickle stays False
+    meta = json.loads(str(z["meta"]))
+    if "env_f32" in z.files:
+        env = z["env_f32"]
+    elif meta["env"]:
+        env = env_png
+    else:
+        env = None
+    return dict(planes=z["planes"], lights=z["lights"], meta=meta, expected=z["expected"], coverage=z["coverage"],
+                sky=z["sky_u16"], env=env)
 
 
 def load_golden(name):

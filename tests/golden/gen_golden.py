@@ -5,7 +5,12 @@ Each fixture holds a small SoA G-buffer, a light list, the pass constants and th
 C++ (oracle/ref_harness.cpp) -- for the same inputs. The fixtures pin ``oracle/pbr_oracle.c``
 (tests/test_oracle_golden.py) on machines where /root/reference is absent (the GPU box).
 
-    make -C oracle all ref && python tests/golden/gen_golden.py
+    make -C oracle all ref && python tests/golden/gen_golden.py            # everything
+    python tests/golden/gen_golden.py --frames                              # frame_*.npz only
+
+The frame_* fixtures cover pbr_shade_frame: a coverage plane with background pixels (the sky pass of
+Skybox.hlsl:37-49 on a procedural sky texture), R8G8B8A8_UNORM output, and an fp32 HDR environment.
+They hold the textures they use (uint16 UNORM or float32 RGBA) next to the planes.
 """
 from __future__ import annotations
 
@@ -265,8 +270,69 @@ CASES = {
 }
 
 
+def frame_planes(rng, h, frac_background):
+    """A G-buffer with background pixels: coverage 0 there, and the normal planes carry the sky
+    direction (some exactly at the poles and on the atan2 seam)."""
+    p = empty_planes(h, W)
+    p[0:3] = random_points(rng, h, W, (-10, -10, 0), (10, 10, 10))
+    p[3:6] = unit(rng.uniform(-1, 1, (3, h, W))).astype(np.float32)
+    p[6:11] = rng.uniform(0, 1, (5, h, W)).astype(np.float32)
+    cov = (rng.uniform(size=(h, W)) >= frac_background).astype(np.uint8)
+    cov[:, :8] = 0  # a fully-background column band
+    sky_dirs = rng.normal(size=(3, h, W)) * rng.uniform(0.1, 50.0, (1, h, W))  # unnormalised, as interpolated
+    sky_dirs[:, 0, :4] = np.array([[0.0, 1.0, 0.0], [0.0, -2.0, 0.0], [-3.0, 0.0, 0.0], [-1.0, 0.5, -0.0]]).T
+    p[3:6] = np.where(cov[None] == 0, sky_dirs, p[3:6]).astype(np.float32)
+    return p, cov
+
+
+def frame_sky_scene(rng):
+    p, cov = frame_planes(rng, 16, 0.35)
+    lights = REF_DIR_LIGHTS + rand_lights(rng, 8, "point")
+    return p, cov, lights, O.OraclePass(n_dir=4, n_point=8, ambient_mode=O.AMBIENT_IBL_DIFFUSE)
+
+
+def hdr_env(w=64, h=32):
+    """A synthetic HDR environment (values up to ~40): the procedural sky scaled, fp32."""
+    sky = envmap.procedural_sky_rgba16(w, h, seed=11).astype(np.float32) / 65535.0
+    sky[..., :3] = sky[..., :3] ** 3 * 40.0
+    sky[..., 3] = 1.0
+    return sky.astype(np.float32)
+
+
+FRAME_CASES = {  # name -> (scene, format, env kind)
+    "frame_sky_rgba8": (frame_sky_scene, O.OUTPUT_RGBA8, "png"),
+    "frame_sky_rgba32f": (frame_sky_scene, O.OUTPUT_RGBA32F, "png"),
+    "frame_hdr_env_rgba32f": (frame_sky_scene, O.OUTPUT_RGBA32F, "hdr"),
+}
+
+
+def make_frames():
+    env_png = envmap.load_chelsea_stairs_env()
+    sky = envmap.procedural_sky_rgba16(96, 48)
+    for k, (name, (fn, fmt, env_kind)) in enumerate(FRAME_CASES.items()):
+        rng = np.random.default_rng(2000 + k)
+        planes, cov, lights, ps = fn(rng)
+        planes = planes.astype(np.float32)
+        lights = np.asarray(lights, np.float32).reshape(-1, 12)
+        env = env_png if env_kind == "png" else hdr_env()
+        expected = O.shade_frame_ref(list(planes), ps, lights, env, sky, cov, fmt)
+        meta = dict(eye=list(ps.eye), ambient=list(ps.ambient), fresnel_r0=list(ps.fresnel_r0),
+                    opacity=ps.opacity, n_dir=ps.n_dir, n_point=ps.n_point, n_spot=ps.n_spot,
+                    ambient_mode=ps.ambient_mode, use_f0_plane=bool(ps.use_f0_plane),
+                    apply_ao=bool(ps.apply_ao), env="Chelsea_Stairs_Env.png" if env_kind == "png" else "",
+                    format=int(fmt))
+        extra = {} if env_kind == "png" else {"env_f32": env}
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), planes=planes, lights=lights, expected=expected,
+                            coverage=cov, sky_u16=sky, meta=np.array(json.dumps(meta)), **extra)
+        print(f"{name:32s} {planes.shape[1] * planes.shape[2]:6d} px  background={int((cov == 0).sum())}")
+
+
 def main():
     if not O.ref_available():
+        sys.exit("oracle/_ref/libpbr_ref.so missing: make -C oracle ref (needs /root/reference)")
+    if "--frames" in sys.argv:
+        make_frames()
+        return
         sys.exit("oracle/_ref/libpbr_ref.so missing: make -C oracle ref (needs /root/reference)")
     env = envmap.load_chelsea_stairs_env()
     for k, (name, fn) in enumerate(CASES.items()):
@@ -284,6 +350,7 @@ def main():
                             expected=expected, meta=np.array(json.dumps(meta)))
         print(f"{name:32s} {planes.shape[1] * planes.shape[2]:6d} px  lights={lights.shape[0]:3d}  "
               f"nan={int(np.isnan(expected).any(axis=-1).sum())}")
+    make_frames()
 
 
 if __name__ == "__main__":

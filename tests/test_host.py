@@ -1,6 +1,7 @@
 """Host-side logic: G-buffer fill determinism and partition independence, scene constants,
 env-map ingest, row-band partitioning."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -151,3 +152,55 @@ def test_libm_port_matches_host_glibc(tmp_path):
     out = subprocess.run([exe, "--quick"], check=True, capture_output=True, text=True).stdout
     print(out)
     assert out.count("mismatches 0") == 7, out
+
+
+def _rgbe_expected(rgbe):
+    e = rgbe[..., 3].astype(np.int64)
+    return np.where(e[..., None] > 0, rgbe[..., :3].astype(np.float64) * np.ldexp(1.0, e[..., None] - 136),
+                    0.0).astype(np.float32)
+
+
+@pytest.mark.parametrize("w", [8, 37, 300])
+def test_hdr_rle_decode_known_answer(w):
+    """RGBE decode (c = mantissa * 2^(e-136), e = 0 -> 0) through new-style RLE scanlines with runs,
+    literals and run/literal boundaries."""
+    rng = np.random.default_rng(w)
+    rgbe = rng.integers(0, 256, (6, w, 4)).astype(np.uint8)
+    rgbe[1, :] = rgbe[1, :1]  # whole-row runs
+    rgbe[2, ::3, 3] = 0  # zero exponents
+    rgbe[3, : w // 2] = rgbe[3, :1]
+    out = envmap.decode_hdr_rgba32f(envmap.encode_hdr_rle(rgbe))
+    assert out.shape == (6, w, 4) and out.dtype == np.float32
+    assert np.array_equal(out[..., :3], _rgbe_expected(rgbe)) and (out[..., 3] == 1.0).all()
+
+
+def test_hdr_flat_and_bad_inputs():
+    rgbe = np.array([[[128, 64, 32, 129], [255, 0, 1, 0], [1, 2, 3, 200]]], np.uint8)  # w = 3 < 8: flat rows
+    data = b"#?RGBE\nGAMMA=1\n\n-Y 1 +X 3\n" + rgbe.tobytes()
+    out = envmap.decode_hdr_rgba32f(data)
+    assert np.array_equal(out[..., :3], _rgbe_expected(rgbe))
+    assert out[0, 0, 0] == 1.0  # 128 * 2^(129-136)
+    for bad in (b"P6\n", b"#?RADIANCE\nFORMAT=32-bit_rle_xyze\n\n-Y 1 +X 3\n" + rgbe.tobytes(),
+                b"#?RADIANCE\n\n+Y 1 +X 3\n" + rgbe.tobytes(), b"#?RADIANCE\n\n-Y 2 +X 3\n" + rgbe.tobytes()):
+        with pytest.raises(ValueError):
+            envmap.decode_hdr_rgba32f(bad)
+
+
+REF_HDR = "/root/reference/Assets/Chelsea_Stairs/Chelsea_Stairs_Env.hdr"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_HDR), reason="reference assets only in the build container")
+def test_hdr_decodes_reference_env_asset():
+    """The reference's Chelsea_Stairs_Env.hdr (read in place, never copied): 360x180, HDR range, and
+    spatially the same image as the 16-bit PNG the IBL path samples."""
+    hdr = envmap.decode_hdr_rgba32f(REF_HDR)
+    png = envmap.load_chelsea_stairs_env().astype(np.float64) / 65535.0
+    assert hdr.shape == (180, 360, 4) and np.isfinite(hdr).all()
+    assert hdr[..., :3].max() > 10.0 and hdr[..., :3].min() >= 0.0
+    assert np.corrcoef(hdr[..., 1].ravel(), png[..., 1].ravel())[0, 1] > 0.5
+
+
+def test_procedural_sky_is_deterministic_unorm16():
+    a, b = envmap.procedural_sky_rgba16(64, 32), envmap.procedural_sky_rgba16(64, 32)
+    assert a.dtype == np.uint16 and a.shape == (32, 64, 4) and np.array_equal(a, b)
+    assert (a[..., 3] == 65535).all() and a[..., :3].std() > 1000

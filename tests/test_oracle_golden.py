@@ -8,7 +8,7 @@ inputs (this container only; the GPU box has no reference).
 import numpy as np
 import pytest
 
-from conftest import golden_names, load_golden, oracle_pass_from_meta
+from conftest import frame_golden_names, golden_names, load_frame_golden, load_golden, oracle_pass_from_meta
 from oracle import oracle as O
 
 
@@ -62,3 +62,59 @@ def test_oracle_matches_reference_build_random(counts, mode, f0, ao, env_map):
     a = O.shade(list(p), ps, lights, env, n_threads=2)
     b = O.shade_ref(list(p), ps, lights, env)
     assert O.bit_equal(a, b).all()
+
+
+@pytest.mark.parametrize("name", frame_golden_names())
+def test_oracle_matches_frame_golden(name, env_map):
+    """pbr_shade_frame's oracle (sky pass, RGBA8, HDR env) against the reference build's output."""
+    g = load_frame_golden(name, env_map)
+    ps = oracle_pass_from_meta(g["meta"])
+    got = O.shade_frame(list(g["planes"]), ps, g["lights"], g["env"], g["sky"], g["coverage"], g["meta"]["format"],
+                        n_threads=3)
+    if g["meta"]["format"] == O.OUTPUT_RGBA8:
+        assert got.dtype == np.uint8 and np.array_equal(got, g["expected"])
+    else:
+        assert O.bit_equal(got, g["expected"]).all()
+    bg = g["coverage"] == 0
+    assert bg.any() and (~bg).any()
+    if g["meta"]["format"] == O.OUTPUT_RGBA32F:
+        assert (got[bg][:, 3] == 1.0).all()  # Skybox.hlsl:49 alpha
+
+
+def test_frame_without_coverage_equals_shade(env_map):
+    """oracle_shade_frame with no coverage plane and RGBA32F output is oracle_shade."""
+    planes, lights, meta, expected = load_golden("mixed_ibl_ao")
+    ps = oracle_pass_from_meta(meta)
+    got = O.shade_frame(list(planes), ps, lights, env_map, None, None, O.OUTPUT_RGBA32F, n_threads=2)
+    assert O.bit_equal(got, expected).all()
+
+
+def test_unorm8_known_answers():
+    """D3D FLOAT -> UNORM8: NaN -> 0, clamp, c*255 + 0.5 (fp32), truncate."""
+    # one ulp below 0.5/255: c*255 = 0.49999997, + 0.5 rounds to 1.0 in fp32 -> 1 (not 0)
+    c = np.array([np.nan, -np.inf, -1.0, -0.0, 0.0, 0.5 / 255, np.nextafter(np.float32(0.5 / 255), np.float32(0)),
+                  1.5 / 255, 0.5, 1.0, 2.0, np.inf, 254.5 / 255, 0.49996], np.float32)
+    want = [0, 0, 0, 0, 0, 1, 1, 2, 128, 255, 255, 255, 255, 127]
+    got = O.unorm8(c)
+    assert got.tolist() == want, got.tolist()
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref needs /root/reference (build container only)")
+@pytest.mark.parametrize("fmt", [O.OUTPUT_RGBA32F, O.OUTPUT_RGBA8])
+def test_frame_oracle_matches_reference_build_random(fmt, env_map):
+    rng = np.random.default_rng(99 + fmt)
+    h, w = 24, 48
+    p = np.zeros((O.NUM_PLANES, h, w), np.float32)
+    p[0:3] = rng.uniform(-30, 30, (3, h, w))
+    n = rng.normal(size=(3, h, w))
+    p[3:6] = n / np.linalg.norm(n, axis=0) * rng.uniform(0.5, 3.0, (1, h, w))
+    p[6:15] = rng.uniform(-0.1, 1.2, (9, h, w))
+    cov = (rng.uniform(size=(h, w)) > 0.5).astype(np.uint8)
+    sky = rng.uniform(0, 5, (20, 40, 4)).astype(np.float32)  # an fp32 HDR sky
+    lights = np.zeros((6, 12), np.float32)
+    lights[:, 0:3] = rng.uniform(0, 80, (6, 3))
+    lights[:, 8:11] = rng.uniform(-40, 40, (6, 3))
+    ps = O.OraclePass(n_point=6, ambient_mode=1)
+    a = O.shade_frame(list(p), ps, lights, env_map, sky, cov, fmt, n_threads=2)
+    b = O.shade_frame_ref(list(p), ps, lights, env_map, sky, cov, fmt)
+    assert (np.array_equal(a, b) if fmt == O.OUTPUT_RGBA8 else O.bit_equal(a, b).all())
