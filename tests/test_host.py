@@ -204,3 +204,16 @@ def test_procedural_sky_is_deterministic_unorm16():
     a, b = envmap.procedural_sky_rgba16(64, 32), envmap.procedural_sky_rgba16(64, 32)
     assert a.dtype == np.uint16 and a.shape == (32, 64, 4) and np.array_equal(a, b)
     assert (a[..., 3] == 65535).all() and a[..., :3].std() > 1000
+
+
+def test_png_writer_round_trips_through_decoder(tmp_path):
+    from physically_based_renderer_amd import image_io
+
+    rng = np.random.default_rng(4)
+    img = rng.integers(0, 256, (7, 13, 4)).astype(np.uint8)
+    path = str(tmp_path / "f.png")
+    image_io.write_png_rgba8(path, img)
+    back = envmap.decode_png_rgba16(path)
+    assert np.array_equal(back, img.astype(np.uint16) * 257)  # exact UNORM8 -> UNORM16 widening
+    with pytest.raises(ValueError):
+        image_io.encode_png_rgba8(img.astype(np.float32))
