@@ -46,14 +46,15 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def bytes_per_pixel(pc) -> int:
-    """Algorithmic HBM bytes per shaded pixel: the planes the kernel reads + the RGBA fp32 write."""
+def bytes_per_pixel(pc, out_bytes: int = 16) -> int:
+    """Algorithmic HBM bytes per shaded pixel: the planes the kernel reads + the RGBA write
+    (16 B fp32, 4 B RGBA8)."""
     planes = 11  # pos xyz, normal xyz, albedo rgb, metallic, roughness
     if pc.flags & N.PBR_FLAG_APPLY_AO:
         planes += 1
     if pc.flags & N.PBR_FLAG_F0_PLANE:
         planes += 3
-    return planes * 4 + 16
+    return planes * 4 + out_bytes
 
 
 def flops_per_pixel(pc) -> int:
@@ -95,11 +96,17 @@ def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int):
     ref = O.shade(list(sample), ops, pc.light_array(), env, n_threads=n_threads)
     dt = time.perf_counter() - t0
     px = sample.shape[1] * sample.shape[2]
+    # single-thread rate on the first 8 sampled rows (single-thread and all-core)
+    one = np.ascontiguousarray(sample[:, :8])
+    t1 = time.perf_counter()
+    O.shade(list(one), ops, pc.light_array(), env, n_threads=1)
+    st = one.shape[1] * one.shape[2] / (time.perf_counter() - t1) / 1e6
     got = gpu_frame[::step]
     err = O.rel_err(got, ref)
     exact = float(O.bit_equal(got, ref).mean())
     return {
         "value": round(px / dt / 1e6, 4), "unit": "Mpix/s", "cores": n_threads, "kind": "port",
+        "single_thread_value": round(st, 4),
         "sample": (f"every {step}th row of" if step > 1 else "all rows of") +
                   f" the same {cfg.width}x{cfg.height} frame ({px} px, {dt:.2f} s wall), "
                   f"oracle/pbr_oracle.c, -O2 -ffp-contract=off, {n_threads} pthreads",
@@ -116,6 +123,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the benchmark); gloo = host-staged gather, for exercising the "
                          "multi-rank path on one GPU")
+    ap.add_argument("--output", default="rgba32f", choices=["rgba32f", "rgba8"],
+                    help="output format: fp32 RGBA (the metric's) or the reference's R8G8B8A8_UNORM back buffer "
+                         "(fused conversion; 4x smaller multi-GPU gather)")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="rows in the CPU-baseline sample (0 = the whole frame: ~1.5 s on 16 host threads)")
     args = ap.parse_args()
@@ -161,8 +171,11 @@ def main():
     log(f"rank {rank}/{world}: {workload} rows [{band.row_begin},{band.row_end}) fill {t_fill:.2f}s "
         f"upload {t_upload * 1e3:.1f} ms ({staging.numel() * 4 / t_upload / 1e9:.1f} GB/s H2D)")
 
-    outs = [torch.empty((band.rows_max, cfg.width, 4), dtype=torch.float32, device=device) for _ in range(2)]
-    gather = D.BandGather(band, cfg.width, device) if world > 1 else None
+    rgba8 = args.output == "rgba8"
+    out_dtype = torch.uint8 if rgba8 else torch.float32
+    fmt = N.PBR_OUTPUT_RGBA8_UNORM if rgba8 else N.PBR_OUTPUT_RGBA32F
+    outs = [torch.empty((band.rows_max, cfg.width, 4), dtype=out_dtype, device=device) for _ in range(2)]
+    gather = D.BandGather(band, cfg.width, device, dtype=out_dtype) if world > 1 else None
     stream = torch.cuda.current_stream(device)
     pending = [[], []]
 
@@ -171,7 +184,10 @@ def main():
         D.BandGather.wait(pending[slot])  # the gather that last read this slot (stream-side wait)
         if ev is not None:
             ev[0].record(stream)
-        ctx.shade(gb, outs[slot], stream)
+        if rgba8:
+            ctx.shade_frame(gb, outs[slot], fmt=fmt, stream=stream)
+        else:
+            ctx.shade(gb, outs[slot], stream)
         if ev is not None:
             ev[1].record(stream)
         if gather is not None:
@@ -200,18 +216,35 @@ def main():
     elapsed = time.perf_counter() - t_start
     kernel_ms = [a.elapsed_time(b) for a, b in events]
 
+    cull_note = {}
+    if pc.flags & N.PBR_FLAG_TILED_CULLING:
+        kept, tiles = ctx.cull_stats(stream)  # of the last timed pass
+        cull_note = {"lights_per_tile": round(kept / max(tiles, 1), 3), "tiles": tiles}
+
     gather_ok = None
+    gather_ms = None
     if world > 1:
+        # The gather alone (no shading), timed the same way: the exchange cost the pipelined step hides.
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter()
+        for k in range(args.steps):
+            D.BandGather.wait(gather.start(outs[k % 2]))
+        torch.cuda.synchronize()
+        dist.barrier()
+        gather_ms = (time.perf_counter() - tg) / args.steps * 1e3
         # Property check of the assembled image: each rank's band checksum (int64 sum of the fp32 bit
         # patterns, exact) must equal the checksum of the slot rank 0 received.
-        last = outs[(args.steps - 1) % 2][: band.rows]
+        last = outs[(args.steps - 1) % 2][: band.rows].contiguous()
+        if rgba8:
+            last = last.view(torch.int32).squeeze(-1)
         coll_dev = device if args.dist_backend == "nccl" else "cpu"
         mine = last.view(torch.int32).to(torch.int64).sum().reshape(1).to(coll_dev)
         sums = [torch.zeros(1, dtype=torch.int64, device=coll_dev) for _ in range(world)]
         dist.all_gather(sums, mine)
         if rank == 0:
-            got = [gather.frame[r, : D.band_rows(cfg.height, world, r).rows].view(torch.int32).to(torch.int64).sum()
-                   for r in range(world)]
+            got = [gather.frame[r, : D.band_rows(cfg.height, world, r).rows].contiguous().view(torch.int32)
+                   .to(torch.int64).sum() for r in range(world)]
             gather_ok = all(int(g.item()) == int(s_.item()) for g, s_ in zip(got, sums))
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=device if args.dist_backend == "nccl" else "cpu")
@@ -223,8 +256,9 @@ def main():
 
     if rank == 0:
         avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+        median_kernel_ms = float(np.median(kernel_ms))
         band_px = cfg.width * band.rows
-        bpp = bytes_per_pixel(pc)
+        bpp = bytes_per_pixel(pc, 4 if rgba8 else 16)
         achieved = bpp * band_px / avg_kernel_s / 1e9
         traffic, valu_busy = load_pmc(workload)
         fpp = flops_per_pixel(pc)
@@ -243,6 +277,7 @@ def main():
             "frac": round(tflops / FP32_PEAK_TFLOPS, 4) if compute_bound else hbm["frac"],
             "traffic": traffic,
             "kernel": "shade_tile_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 4),
+            "median_launch_ms": round(median_kernel_ms, 4),
             "flop_per_px": fpp, "bytes_per_px": bpp, "px_per_launch": band_px,
             "hbm": hbm,
             "valu_issue_busy": valu_busy,
@@ -252,7 +287,7 @@ def main():
         }
         cpu = None
         parity = {}
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not rgba8:
             frame = outs[0][: band.rows].cpu().numpy()
             cpu, max_rel, exact = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows)
             parity = {"parity_max_rel": max_rel, "parity_bit_exact_frac": round(exact, 6)}
@@ -260,11 +295,12 @@ def main():
         if world > 1:
             gather_note = {"gather": ("batched isend/irecv star to rank 0 (RCCL), pipelined with the next frame"
                                       if args.dist_backend == "nccl" else "host-staged gloo gather (test mode)"),
-                           "gather_checksums_match": gather_ok}
+                           "gather_checksums_match": gather_ok, "gather_ms": round(gather_ms, 4),
+                           "shade_ms": round(avg_kernel_s * 1e3, 4)}
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "output": args.output,
             "data": "synthetic deterministic G-buffer (splitmix64 per pixel; rustediron metal/rough tiles; "
                     "Chelsea_Stairs 16-bit env)",
             "config": {"workload": workload, "width": cfg.width, "height": cfg.height,
@@ -275,7 +311,7 @@ def main():
             "hbm_gbps": round(achieved, 2),
             "roofline": roofline,
             "cpu_baseline": cpu,
-            **parity, **gather_note,
+            **parity, **gather_note, **cull_note,
             "pcie_h2d_gbps": round(staging.numel() * 4 / t_upload / 1e9, 2),
         }
         print(json.dumps(out), flush=True)
