@@ -168,8 +168,18 @@ int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num
 typedef enum pbr_scene_kind {
     PBR_SCENE_SPHERE_RUSTEDIRON = 1, /* BASELINE config 1: ray-cast unit sphere, rustediron metal/rough */
     PBR_SCENE_RANDOM_COVERED = 2,    /* configs 2, 3, 5: fully covered synthetic G-buffer */
-    PBR_SCENE_PLANE_MATERIALS = 4    /* config 4: plane y = 0 seen top-down, seven *_1K material sets */
+    PBR_SCENE_PLANE_MATERIALS = 4,   /* config 4: plane y = 0 seen top-down, seven *_1K material sets */
+    PBR_SCENE_REFERENCE_SPHERES = 5  /* the reference's own scene: 49 red spheres + 9 textured spheres
+                                        (PBRApp.cpp:964-973, 1016-1068) under its 4 directional lights */
 } pbr_scene_kind;
+
+/* A left-handed look-at camera with world up (0, 1, 0), like Camera (Camera.cpp:104-112). */
+typedef struct pbr_camera {
+    float eye[3];
+    float target[3];
+    float fov_y; /* radians */
+    float pad0;
+} pbr_camera;
 
 /* Host-side texture tiles the scenes sample (owned by the caller). */
 typedef struct pbr_scene_assets {
@@ -192,6 +202,8 @@ typedef struct pbr_scene_desc {
     int32_t height;       /* never on how rows are partitioned across calls or ranks */
     uint64_t seed;
     const pbr_scene_assets* assets;
+    const pbr_camera* camera; /* kind 5 only; NULL = the reference's initial camera: eye (0, 0, -5) looking
+                                 down +z, fovY pi/4 (BuildCamera, PBRApp.cpp:652-659) */
 } pbr_scene_desc;
 
 /* Fills rows [row_begin, row_end) of the full frame into HOST planes laid out like
@@ -209,7 +221,8 @@ int64_t pbr_gbuffer_fill_coverage(const pbr_scene_desc* scene, int32_t row_begin
                                   int64_t coverage_stride, int32_t n_threads);
 
 /* The light list and pass constants of a benchmark scene (`n_lights` point lights; kind 1 uses one
- * light at (20, 20, -20), strength 100, PBRApp.cpp:490-491). `pass->lights` is set to `lights`. */
+ * light at (20, 20, -20), strength 100, PBRApp.cpp:490-491; kind 5 uses the reference's four
+ * directional lights, PBRApp.cpp:480-487, and needs n_lights == 4). `pass->lights` is set to `lights`. */
 int pbr_scene_pass(const pbr_scene_desc* scene, int32_t n_lights, pbr_light* lights, pbr_pass_desc* pass);
 
 const char* pbr_strerror(int status);

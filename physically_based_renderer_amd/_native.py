@@ -28,6 +28,7 @@ PBR_OUTPUT_RGBA8_UNORM = 1
 PBR_SCENE_SPHERE_RUSTEDIRON = 1
 PBR_SCENE_RANDOM_COVERED = 2
 PBR_SCENE_PLANE_MATERIALS = 4
+PBR_SCENE_REFERENCE_SPHERES = 5
 
 NUM_PLANES = 15
 PLANE_NAMES = ("px", "py", "pz", "nx", "ny", "nz", "ar", "ag", "ab",
@@ -112,6 +113,15 @@ class SceneAssets(ctypes.Structure):
     ]
 
 
+class Camera(ctypes.Structure):
+    _fields_ = [
+        ("eye", ctypes.c_float * 3),
+        ("target", ctypes.c_float * 3),
+        ("fov_y", ctypes.c_float),
+        ("pad0", ctypes.c_float),
+    ]
+
+
 class SceneDesc(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32),
@@ -119,6 +129,7 @@ class SceneDesc(ctypes.Structure):
         ("height", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
         ("assets", ctypes.POINTER(SceneAssets)),
+        ("camera", ctypes.POINTER(Camera)),
     ]
 
 

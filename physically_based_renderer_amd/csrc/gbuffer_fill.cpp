@@ -176,11 +176,171 @@ void fill_plane(const pbr_scene_desc& sc, int y, Row r) {
     }
 }
 
+// ---- Kind 5: the reference scene -------------------------------------------------------------------
+// 49 red spheres in a 7x7 grid (x = (i%7)*2.5 - 7.5, y = -(i/7)*2.5 - 2.5; roughness (i%7)/6, metallic
+// 1 - (i/7)/6, albedo (1,0,0), F0 0.04; PBRApp.cpp:964-973, 1016-1022) and nine textured spheres on
+// y = 0 (PBRApp.cpp:1023-1068), all SphereMesh radius 1 (PBRApp.cpp:515-560), ray-cast analytically
+// from the camera instead of rasterised (the mesh's triangle interpolation is G-buffer content,
+// parity-unpinned like the texture filtering). Per hit: PosW; NormalW = normalize(P - C) (Default.hlsl:50);
+// SphereMesh's frame (Mesh.h:506-523): UV = (theta / 2pi, phi / pi), T = dP/dtheta = (-q.z, 0, q.x),
+// B = cross(N, T) (neither normalised); materials per the reference's permutations (PBRApp.cpp:892-963,
+// Default.hlsl:79-116); N = NormalSampleToWorldSpace (LightingUtil.hlsl:203-214, not renormalised);
+// F0 resolved into the F0 plane (specular map, or lerp(0.04, albedo, metallic)).
+struct RefSphere {
+    float cx, cy;
+    int tile;  // material tile (assets order: brick_modern, concrete_dirty, concrete_rough, grass_wild,
+               // metal_bare, soil_mud, stone_wall), -1 = constant / special
+    int kind;  // 0 red (index in `red`), 1 tiled, 2 rusted iron, 3 rock copper
+    int red;
+};
+
+constexpr int kRefSpheres = 58;
+
+RefSphere ref_sphere(int s) {
+    if (s < 49) return RefSphere{(s % 7) * 2.5f - 3 * 2.5f, (s / 7) * -2.5f - 2.5f, -1, 0, s};
+    static const RefSphere textured[9] = {
+        {0.0f, 0.0f, -1, 2, 0},    // sphere_rust           (rusted_iron: metallic + roughness maps)
+        {-2.5f, 0.0f, -1, 3, 0},   // sphere_rock_copper    (maps not among the committed tiles: constants)
+        {-5.0f, 0.0f, 0, 1, 0},    // sphere_brick_modern
+        {-7.5f, 0.0f, 1, 1, 0},    // sphere_concrete_dirty
+        {-10.0f, 0.0f, 2, 1, 0},   // sphere_concrete_rough
+        {2.5f, 0.0f, 3, 1, 0},     // sphere_grass_wild
+        {5.0f, 0.0f, 4, 1, 0},     // sphere_metal_bare
+        {7.5f, 0.0f, 5, 1, 0},     // sphere_soil_mud
+        {10.0f, 0.0f, 6, 1, 0}};   // sphere_stone_wall
+    return textured[s - 49];
+}
+
+struct Basis {
+    double eye[3], f[3], r[3], u[3], t;
+};
+
+Basis camera_basis(const pbr_scene_desc& sc) {
+    pbr_camera def = {{0.0f, 0.0f, -5.0f}, {0.0f, 0.0f, 0.0f}, (float)(M_PI / 4.0), 0.0f};
+    const pbr_camera& c = sc.camera ? *sc.camera : def;
+    Basis b;
+    double f[3] = {(double)c.target[0] - c.eye[0], (double)c.target[1] - c.eye[1], (double)c.target[2] - c.eye[2]};
+    double fl = std::sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+    for (int i = 0; i < 3; ++i) b.eye[i] = c.eye[i], b.f[i] = f[i] / fl;
+    // left-handed: right = cross(up, forward), up' = cross(forward, right)
+    double r[3] = {b.f[2], 0.0, -b.f[0]};
+    double rl = std::sqrt(r[0] * r[0] + r[2] * r[2]);
+    for (int i = 0; i < 3; ++i) b.r[i] = r[i] / rl;
+    b.u[0] = b.f[1] * b.r[2] - b.f[2] * b.r[1];
+    b.u[1] = b.f[2] * b.r[0] - b.f[0] * b.r[2];
+    b.u[2] = b.f[0] * b.r[1] - b.f[1] * b.r[0];
+    b.t = std::tan(0.5 * (double)c.fov_y);
+    return b;
+}
+
+void fill_reference(const pbr_scene_desc& sc, int y, Row r) {
+    const pbr_scene_assets* as = sc.assets;
+    const Basis b = camera_basis(sc);
+    const double aspect = (double)sc.width / (double)sc.height;
+    const int T = as->mat_size, RS = as->rust_size;
+    for (int x = 0; x < sc.width; ++x) {
+        const double sx = (2.0 * (x + 0.5) / sc.width - 1.0) * b.t * aspect, sy = (1.0 - 2.0 * (y + 0.5) / sc.height) * b.t;
+        double d[3];
+        for (int i = 0; i < 3; ++i) d[i] = b.f[i] + sx * b.r[i] + sy * b.u[i];
+        const double dl = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+        for (int i = 0; i < 3; ++i) d[i] /= dl;
+        // nearest hit within the camera's [near, far] = [0.1, 100] (BuildCamera, PBRApp.cpp:654)
+        double best = 100.0;
+        int hit = -1;
+        for (int s = 0; s < kRefSpheres; ++s) {
+            const RefSphere sp = ref_sphere(s);
+            const double o[3] = {b.eye[0] - sp.cx, b.eye[1] - sp.cy, b.eye[2]};
+            const double bb = o[0] * d[0] + o[1] * d[1] + o[2] * d[2];
+            const double cc = o[0] * o[0] + o[1] * o[1] + o[2] * o[2] - 1.0;
+            const double disc = bb * bb - cc;
+            if (disc < 0.0) continue;
+            const double sq = std::sqrt(disc);
+            double tt = -bb - sq;
+            if (tt < 0.1) tt = -bb + sq;  // eye inside / behind the near plane: the far side
+            if (tt >= 0.1 && tt < best) best = tt, hit = s;
+        }
+        set_cov(r, x, hit >= 0);
+        r.p[kAo][x] = 1.0f;
+        if (hit < 0) {  // background: the view direction for the sky pass (Skybox.hlsl:24, 41)
+            r.p[kPosX][x] = (float)(b.eye[0] + d[0] * 100.0);
+            r.p[kPosY][x] = (float)(b.eye[1] + d[1] * 100.0);
+            r.p[kPosZ][x] = (float)(b.eye[2] + d[2] * 100.0);
+            r.p[kNx][x] = (float)d[0];
+            r.p[kNy][x] = (float)d[1];
+            r.p[kNz][x] = (float)d[2];
+            r.p[kAr][x] = r.p[kAg][x] = r.p[kAb][x] = 0.0f;
+            r.p[kMetal][x] = 0.0f;
+            r.p[kRough][x] = 1.0f;
+            r.p[kF0r][x] = r.p[kF0g][x] = r.p[kF0b][x] = 0.04f;
+            continue;
+        }
+        const RefSphere sp = ref_sphere(hit);
+        const double P[3] = {b.eye[0] + d[0] * best, b.eye[1] + d[1] * best, b.eye[2] + d[2] * best};
+        const double q[3] = {P[0] - sp.cx, P[1] - sp.cy, P[2]};
+        const double ql = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+        const float nw[3] = {(float)(q[0] / ql), (float)(q[1] / ql), (float)(q[2] / ql)};
+        r.p[kPosX][x] = (float)P[0];
+        r.p[kPosY][x] = (float)P[1];
+        r.p[kPosZ][x] = (float)P[2];
+        double theta = std::atan2(q[2], q[0]);
+        if (theta < 0.0) theta += 2.0 * M_PI;
+        const double uu = theta / (2.0 * M_PI), vv = std::acos(std::fmin(std::fmax(q[1] / ql, -1.0), 1.0)) / M_PI;
+        const float tg[3] = {(float)-q[2], 0.0f, (float)q[0]};  // dP/dtheta
+        const float bt[3] = {nw[1] * tg[2] - nw[2] * tg[1], nw[2] * tg[0] - nw[0] * tg[2], nw[0] * tg[1] - nw[1] * tg[0]};
+        float alb[3], f0[3], metal, rough, n[3] = {nw[0], nw[1], nw[2]};
+        bool has_spec = false;
+        if (sp.kind == 0) {  // textureless red sphere (PBRApp.cpp:964-973)
+            alb[0] = 1.0f, alb[1] = 0.0f, alb[2] = 0.0f;
+            rough = (float)(sp.red % 7) / 6.0f;
+            metal = 1.0f - (float)(sp.red / 7) / 6.0f;
+        } else if (sp.kind == 2) {  // rusted iron: metallic + roughness maps (basecolor/normal absent, F6)
+            const int tx = std::min(RS - 1, (int)(uu * RS)), ty = std::min(RS - 1, (int)(vv * RS));
+            alb[0] = alb[1] = alb[2] = 0.5f;
+            metal = (float)as->rust_metallic[(size_t)ty * RS + tx] / 255.0f;
+            rough = (float)as->rust_roughness[(size_t)ty * RS + tx] / 255.0f;
+        } else if (sp.kind == 3) {  // rock copper: constant copper-like values (maps not committed)
+            alb[0] = 0.95f, alb[1] = 0.64f, alb[2] = 0.54f;
+            metal = 1.0f;
+            rough = 0.35f;
+        } else {
+            const int tx = std::min(T - 1, (int)(uu * T)), ty = std::min(T - 1, (int)(vv * T));
+            const size_t t = ((size_t)sp.tile * T + (size_t)ty) * T + (size_t)tx;
+            const uint8_t* a = as->mat_albedo + 3 * t;
+            const uint8_t* sv = as->mat_specular + 3 * t;
+            const uint8_t* nm = as->mat_normal + 3 * t;
+            for (int c = 0; c < 3; ++c) alb[c] = a[c] / 255.0f, f0[c] = sv[c] / 255.0f;
+            has_spec = true;
+            rough = as->mat_roughness[t] / 255.0f;
+            metal = as->mat_has_metallic[sp.tile] ? as->mat_metallic[t] / 255.0f : 0.0f;  // g_Metallic = 0
+            const float nt[3] = {2.0f * (nm[0] / 255.0f) - 1.0f, 2.0f * (nm[1] / 255.0f) - 1.0f,
+                                 2.0f * (nm[2] / 255.0f) - 1.0f};
+            for (int c = 0; c < 3; ++c) n[c] = nt[0] * tg[c] + nt[1] * bt[c] + nt[2] * nw[c];  // mul(normalT, TBN)
+        }
+        if (!has_spec)
+            for (int c = 0; c < 3; ++c) f0[c] = lerp_h(0.04f, alb[c], metal);  // Default.hlsl:94-95
+        r.p[kNx][x] = n[0];
+        r.p[kNy][x] = n[1];
+        r.p[kNz][x] = n[2];
+        r.p[kAr][x] = alb[0];
+        r.p[kAg][x] = alb[1];
+        r.p[kAb][x] = alb[2];
+        r.p[kMetal][x] = metal;
+        r.p[kRough][x] = rough;
+        r.p[kF0r][x] = f0[0];
+        r.p[kF0g][x] = f0[1];
+        r.p[kF0b][x] = f0[2];
+    }
+}
+
 bool assets_ok(const pbr_scene_desc* sc) {
     const pbr_scene_assets* as = sc->assets;
     if (!as) return false;
     if (sc->kind == PBR_SCENE_SPHERE_RUSTEDIRON || sc->kind == PBR_SCENE_RANDOM_COVERED)
         return as->rust_metallic && as->rust_roughness && as->rust_size > 0;
+    if (sc->kind == PBR_SCENE_REFERENCE_SPHERES)
+        return as->rust_metallic && as->rust_roughness && as->rust_size > 0 && as->mat_albedo && as->mat_specular &&
+               as->mat_roughness && as->mat_metallic && as->mat_has_metallic && as->mat_normal &&
+               as->num_materials >= 7 && as->mat_size > 0;
     if (sc->kind == PBR_SCENE_PLANE_MATERIALS)
         return as->mat_albedo && as->mat_specular && as->mat_roughness && as->mat_metallic && as->mat_has_metallic &&
                as->mat_normal && as->num_materials > 0 && as->mat_size > 0;
@@ -219,9 +379,18 @@ extern "C" int64_t pbr_gbuffer_fill_coverage(const pbr_scene_desc* scene, int32_
             switch (scene->kind) {
                 case PBR_SCENE_SPHERE_RUSTEDIRON: covered[t] += fill_sphere(*scene, y, r); break;
                 case PBR_SCENE_RANDOM_COVERED: fill_random_covered(*scene, y, r); covered[t] += scene->width; break;
+                case PBR_SCENE_REFERENCE_SPHERES: {
+                    Row rc = r;
+                    std::vector<uint8_t> tmp;
+                    if (!rc.cov) tmp.resize((size_t)scene->width), rc.cov = tmp.data();
+                    fill_reference(*scene, y, rc);
+                    for (int x = 0; x < scene->width; ++x) covered[t] += rc.cov[x];
+                    break;
+                }
                 default: fill_plane(*scene, y, r); covered[t] += scene->width; break;
             }
-            if (r.cov && scene->kind != PBR_SCENE_SPHERE_RUSTEDIRON) std::memset(r.cov, 1, (size_t)scene->width);
+            if (r.cov && scene->kind != PBR_SCENE_SPHERE_RUSTEDIRON && scene->kind != PBR_SCENE_REFERENCE_SPHERES)
+                std::memset(r.cov, 1, (size_t)scene->width);
         }
     };
     std::vector<std::thread> th;
@@ -249,6 +418,21 @@ extern "C" int pbr_scene_pass(const pbr_scene_desc* scene, int32_t n_lights, pbr
     pass->ambient_mode = PBR_AMBIENT_CONSTANT;
     pass->num_point_lights = n_lights;
     pass->lights = lights;
+    if (scene->kind == PBR_SCENE_REFERENCE_SPHERES) {  // PBRApp.cpp:480-487: four directional lights
+        if (n_lights != 4) return PBR_ERR_INVALID_ARGUMENT;
+        static const float dirs[4][3] = {{0.57735f, 0.57735f, 0.57735f}, {0.57735f, -0.57735f, 0.57735f},
+                                         {-0.57735f, 0.57735f, 0.57735f}, {-0.57735f, -0.57735f, 0.57735f}};
+        for (int i = 0; i < 4; ++i) {
+            std::memset(&lights[i], 0, sizeof(pbr_light));
+            lights[i].spot_power = 64.0f;
+            for (int c = 0; c < 3; ++c) lights[i].strength[c] = 0.25f, lights[i].direction[c] = dirs[i][c];
+        }
+        pass->num_point_lights = 0;
+        pass->num_dir_lights = 4;
+        if (scene->camera)
+            for (int c = 0; c < 3; ++c) pass->eye_pos_w[c] = scene->camera->eye[c];
+        return PBR_OK;
+    }
     const uint64_t ls = scene->seed ^ kLightStream;
     const float s = 1000.0f / (float)(scene->height > 0 ? scene->height : 1);
     const float half_w = 0.5f * (float)scene->width * s;

@@ -6,6 +6,9 @@
     4  3840x2160, 256 point lights, tiled light culling, *_1K materials, F0 plane
     5  8192x8192, 64 point lights + IBL, row bands across GPUs + RCCL gather
 
+plus REFERENCE_SCENE: the reference's own 58-sphere scene under its 4 directional lights,
+ray-cast from a camera, with background pixels for the sky pass.
+
 All inputs are synthetic but deterministic functions of (global pixel, seed); see DESIGN.md.
 """
 from __future__ import annotations
@@ -35,9 +38,13 @@ class SceneConfig:
     ambient_mode: int
     flags: int
     seed: int
+    camera: Optional[tuple] = None  # (eye xyz, target xyz, fov_y) for the reference scene; None = its default
 
     def with_size(self, width: int, height: int) -> "SceneConfig":
         return replace(self, width=width, height=height)
+
+    def with_camera(self, eye, target, fov_y: float = float(np.pi / 4)) -> "SceneConfig":
+        return replace(self, camera=(tuple(eye), tuple(target), float(fov_y)))
 
 
 CONFIGS = {
@@ -52,6 +59,14 @@ CONFIGS = {
     5: SceneConfig(5, "cfg5_8192x8192_64pt_ibl_rowbands", N.PBR_SCENE_RANDOM_COVERED, 8192, 8192, 64,
                    N.PBR_AMBIENT_IBL_DIFFUSE, 0, 0x5EED0005),
 }
+
+
+# The reference scene (PBRApp.cpp:964-973, 1016-1068), F0 resolved into the plane by the fill. Its
+# default camera is BuildCamera's (eye (0, 0, -5) looking down +z, PBRApp.cpp:652-659); OVERVIEW_CAMERA
+# backs off to show all 58 spheres.
+REFERENCE_SCENE = SceneConfig(0, "reference_58_spheres", N.PBR_SCENE_REFERENCE_SPHERES, 1280, 720, 4,
+                              N.PBR_AMBIENT_CONSTANT, N.PBR_FLAG_F0_PLANE, 0x5EED0000)
+OVERVIEW_CAMERA = ((0.0, -7.0, -30.0), (0.0, -7.0, 0.0), float(np.pi / 4))
 
 
 class Assets:
@@ -97,6 +112,13 @@ def _scene_desc(cfg: SceneConfig, assets: Assets) -> N.SceneDesc:
     d = N.SceneDesc()
     d.kind, d.width, d.height, d.seed = cfg.kind, cfg.width, cfg.height, cfg.seed
     d.assets = ctypes.pointer(assets.c)
+    if cfg.camera is not None:
+        cam = N.Camera()
+        cam.eye[:] = [float(v) for v in cfg.camera[0]]
+        cam.target[:] = [float(v) for v in cfg.camera[1]]
+        cam.fov_y = float(cfg.camera[2])
+        d._camera_keep = cam  # the pointer below must not outlive it
+        d.camera = ctypes.pointer(cam)
     return d
 
 

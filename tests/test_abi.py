@@ -36,12 +36,36 @@ def test_library_is_built_for_gfx950():
     assert b"gfx950" in blob
 
 
-def test_struct_layouts_match_header():
-    assert ctypes.sizeof(N.Light) == 48  # LightingUtil.hlsl:9-17
-    assert N.Light.position.offset == 32
-    assert ctypes.sizeof(N.GBufferSoA) == 15 * 8 + 8 + 8
-    assert N.PassDesc.lights.offset == 64
-    assert ctypes.sizeof(N.SceneDesc) == 24 + 8
+STRUCTS = {  # C struct -> ctypes mirror
+    "pbr_light": "Light", "pbr_pass_desc": "PassDesc", "pbr_gbuffer_soa": "GBufferSoA",
+    "pbr_frame_desc": "FrameDesc", "pbr_scene_assets": "SceneAssets", "pbr_camera": "Camera",
+    "pbr_scene_desc": "SceneDesc",
+}
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Every ctypes mirror has the size and field offsets the C compiler gives the header's struct."""
+    assert ctypes.sizeof(N.Light) == 48 and N.Light.position.offset == 32  # LightingUtil.hlsl:9-17
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "pbr/pbr_shade.h"', "int main(void) {"]
+    for cs, py in STRUCTS.items():
+        lines.append(f'printf("{cs} size %zu\\n", sizeof({cs}));')
+        for name, *_ in getattr(N, py)._fields_:
+            lines.append(f'printf("{cs} {name} %zu\\n", offsetof({cs}, {name}));')
+    lines += ["return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = str(tmp_path / "layout")
+    inc = os.path.join(os.path.dirname(N.HEADER_PATH), "..")
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", exe], check=True)
+    c_layout = {}
+    for line in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.splitlines():
+        cs, name, v = line.split()
+        c_layout[(cs, name)] = int(v)
+    for cs, py in STRUCTS.items():
+        cls = getattr(N, py)
+        assert c_layout[(cs, "size")] == ctypes.sizeof(cls), cs
+        for name, *_ in cls._fields_:
+            assert c_layout[(cs, name)] == getattr(cls, name).offset, f"{cs}.{name}"
 
 
 def test_strerror_and_status_codes():

@@ -171,3 +171,20 @@ def test_frame_error_paths(gpu):
     with pytest.raises(ValueError):
         ctx.set_sky_map(np.zeros((4, 4, 4), np.int32))
     ctx.close()
+
+
+@pytest.mark.parametrize("camera", [None, "overview"])
+def test_reference_scene_frame(camera, shading_ctx, gpu):
+    """The reference's own scene end to end: ray-cast G-buffer with coverage, PS on the
+    58 spheres under the 4 directional lights, sky pass behind, RGBA8 back buffer."""
+    cfg = S.REFERENCE_SCENE.with_size(640, 360)
+    if camera:
+        cfg = cfg.with_camera(*S.OVERVIEW_CAMERA)
+    planes, cov = S.fill_gbuffer_host_coverage(cfg)
+    pc = S.scene_pass(cfg)
+    sky = envmap.procedural_sky_rgba16(256, 128)
+    for fmt in (N.PBR_OUTPUT_RGBA32F, N.PBR_OUTPUT_RGBA8_UNORM):
+        got = run_frame(shading_ctx, gpu, planes, pc, None, sky, cov, fmt)
+        ref = O.shade_frame(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, sky, cov,
+                            O.OUTPUT_RGBA8 if fmt == N.PBR_OUTPUT_RGBA8_UNORM else O.OUTPUT_RGBA32F, n_threads=8)
+        check(got, ref, cov, fmt, f"reference scene camera={camera} fmt={fmt}")

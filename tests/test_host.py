@@ -217,3 +217,31 @@ def test_png_writer_round_trips_through_decoder(tmp_path):
     assert np.array_equal(back, img.astype(np.uint16) * 257)  # exact UNORM8 -> UNORM16 widening
     with pytest.raises(ValueError):
         image_io.encode_png_rgba8(img.astype(np.float32))
+
+
+@pytest.mark.parametrize("camera", [None, "overview"])
+def test_reference_scene_fill(camera):
+    """The 58-sphere reference scene: partition-independent fill with coverage, finite geometry,
+    F0 resolved per material permutation, the reference's four directional lights."""
+    cfg = S.REFERENCE_SCENE.with_size(320, 180)
+    if camera:
+        cfg = cfg.with_camera(*S.OVERVIEW_CAMERA)
+    full, cov = S.fill_gbuffer_host_coverage(cfg, n_threads=3)
+    parts = [S.fill_gbuffer_host_coverage(cfg, r0, r1, n_threads=2) for r0, r1 in [(0, 41), (41, 100), (100, 180)]]
+    assert np.array_equal(np.concatenate([p for p, _ in parts], axis=1).view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(np.concatenate([c for _, c in parts], axis=0), cov)
+    planes, covered = S.fill_gbuffer_host(cfg)
+    assert np.array_equal(planes.view(np.uint32), full.view(np.uint32)) and covered == int(cov.sum())
+    assert 0 < covered < cfg.width * cfg.height and np.isfinite(full).all()
+    g = cov == 1
+    red = g & (full[6] == 1.0) & (full[7] == 0.0) & (full[8] == 0.0)
+    assert red.any()  # textureless red spheres: F0 = lerp(0.04, albedo, metallic) (Default.hlsl:94-95)
+    m = full[9][red]
+    np.testing.assert_array_equal(full[12][red], (np.float32(0.04) + m * (np.float32(1.0) - np.float32(0.04))))
+    bg = ~g  # background normal planes carry the unit view direction
+    nrm = np.sqrt((full[3:6, bg].astype(np.float64) ** 2).sum(0))
+    assert np.allclose(nrm, 1.0, atol=1e-6)
+    pc = S.scene_pass(cfg)
+    assert (pc.num_dir_lights, pc.num_point_lights) == (4, 0) and pc.flags & N.PBR_FLAG_F0_PLANE
+    L = pc.light_array()
+    assert np.allclose(np.abs(L[:, 4:7]), 0.57735) and np.allclose(L[:, 0:3], 0.25)
