@@ -64,14 +64,15 @@ __device__ __forceinline__ float div_nr(float x, Recip d) {
     float t = __builtin_fmaf(d.y, q, -x);
     return __builtin_fmaf(-t, d.r, q);
 }
+// sqrt in five operations: y = v_rsq(x), s0 = x*y, r = x - s0^2 (fma), s = s0 + r*(y/2) (fma). Probed
+// on gfx950 to equal the IEEE sqrtf for every float with exponent in [-64, 64] (tests/hip/sqrt_probe.hip,
+// test_gpu_probes.py); the window checks keep every use inside that range (dist >= 2^-20, |V+L| >= 2^-30;
+// x = 0 gives NaN, which fails them).
 __device__ __forceinline__ float sqrt_nr(float x) {
-    float s = __builtin_amdgcn_sqrtf(x);
-    float sm = __int_as_float(__float_as_int(s) - 1);
-    float sp = __int_as_float(__float_as_int(s) + 1);
-    float rm = __builtin_fmaf(-sm, s, x);
-    float rp = __builtin_fmaf(-sp, s, x);
-    s = (rm <= 0.0f) ? sm : s;
-    return (rp > 0.0f) ? sp : s;
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s0 = x * y;
+    const float r = __builtin_fmaf(-s0, s0, x);
+    return __builtin_fmaf(r, 0.5f * y, s0);
 }
 // |x| in [lo, hi] (false for NaN); zero_or_in also accepts +-0.
 __device__ __forceinline__ bool in_win(float x, float lo, float hi) { return fabsf(x) >= lo && fabsf(x) <= hi; }
@@ -122,6 +123,14 @@ __device__ __forceinline__ float pow5_light(float x) {
 __device__ __forceinline__ float powf_glibc(float x, float y) { return pbr_powf(x, y); }
 
 constexpr float kPi = 3.14159265359f;  // LightingUtil.hlsl:59, 103 (an fp32 literal in HLSL)
+
+// x / kPi in two operations: q = fma(x, zh, x * zl) with zh = RN(1/kPi), zl = RN(1/kPi - zh). Checked
+// exhaustively to equal the IEEE quotient for every significand (tests: test_div_pi_is_exact on the
+// host, fastdiv_probe on the GPU), hence for every |x| in [2^-98, 2^100] or 0, where x * zl stays
+// normal. In the fast-path window kD * albedo is 0 or >= 2^-68 in magnitude (|1-F|, 1-metallic >= 2^-24
+// or 0; albedo >= 2^-20).
+constexpr float kInvPiHi = 0x1.45f306p-2f, kInvPiLo = 0x1.11be6cp-28f;
+__device__ __forceinline__ float div_pi(float x) { return __builtin_fmaf(x, kInvPiHi, x * kInvPiLo); }
 constexpr float kInvGamma = 1.0f / 2.2f;  // Default.hlsl:155
 constexpr float kLightRange = 100.0f;     // LightingUtil.hlsl:131
 
@@ -135,7 +144,6 @@ struct PixelInvariants {
     float k, one_minus_k;   // GeometrySchlickGGX: k = (r+1)^2 / 8 on the unclamped roughness (:66-67)
     float ggx_v;            // GeometrySchlickGGX(NdotV) = ggx2 (:79)
     float four_n_dot_v;     // 4.0f * max(dot(N,V), 0) (:95, left operand of the product)
-    Recip r_pi;             // refined reciprocal of PI for the exact fast division by PI (:103)
     bool fast_ok;           // the pixel's inputs lie in the fast-path window (see below)
     bool f0_nonzero;        // no F0 component is zero
 };
@@ -192,7 +200,6 @@ __device__ __forceinline__ PixelInvariants make_invariants(f3 n, f3 v, f3 albedo
     float n_dot_v = hmax(dot3(n, v), 0.0f);
     q.ggx_v = n_dot_v / (n_dot_v * q.one_minus_k + q.k);
     q.four_n_dot_v = 4.0f * n_dot_v;
-    q.r_pi = recip_nr(kPi);
     q.fast_ok = false;
     q.f0_nonzero = f0_nonzero(f0);
     return q;
@@ -242,10 +249,11 @@ __device__ __forceinline__ f3 brdf_cook_torrance(const PixelInvariants& q, f3 ra
     f3 spec = mk3(qdiv<FAST>(nom.x, rdenom), qdiv<FAST>(nom.y, rdenom), qdiv<FAST>(nom.z, rdenom));
     // kD = (1 - F) * (1 - metallic)
     f3 kd = mk3((1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal);
-    const Recip rpi = FAST ? q.r_pi : Recip{kPi, 0.0f};
-    return mk3(((qdiv<FAST>(kd.x * q.albedo.x, rpi) + spec.x) * radiance.x) * n_dot_l,
-               ((qdiv<FAST>(kd.y * q.albedo.y, rpi) + spec.y) * radiance.y) * n_dot_l,
-               ((qdiv<FAST>(kd.z * q.albedo.z, rpi) + spec.z) * radiance.z) * n_dot_l);
+    const f3 kda = mk3(kd.x * q.albedo.x, kd.y * q.albedo.y, kd.z * q.albedo.z);
+    const f3 diffuse = FAST ? mk3(div_pi(kda.x), div_pi(kda.y), div_pi(kda.z))
+                            : mk3(kda.x / kPi, kda.y / kPi, kda.z / kPi);
+    return mk3(((diffuse.x + spec.x) * radiance.x) * n_dot_l, ((diffuse.y + spec.y) * radiance.y) * n_dot_l,
+               ((diffuse.z + spec.z) * radiance.z) * n_dot_l);
 }
 
 // normalize(v) through the fast path: sqrt_nr + three divisions sharing one refined reciprocal.
@@ -282,7 +290,8 @@ __device__ __forceinline__ bool point_or_spot_light(const PixelInvariants& q, f3
     l = mk3(qdiv<FAST>(l.x, rdist), qdiv<FAST>(l.y, rdist), qdiv<FAST>(l.z, rdist));
     f3 h = normalize_q<FAST>(add3(q.v, l), ok);
     float dsat = hmax(dist, 0.01f);  // CalcAttenuation (:35-40); dsat^2 in [1e-4, 1e4]
-    float att = qdiv<FAST>(1.0f, qrecip<FAST>(dsat * dsat));
+    // 1 / dsat^2: the refined reciprocal is already RN(1/y) in this window (exponents [-14, 14])
+    float att = FAST ? qrecip<FAST>(dsat * dsat).r : 1.0f / (dsat * dsat);
     if (SPOT) {
         f3 nl = mk3(-l.x, -l.y, -l.z);
         att *= powf_glibc(hmax(dot3(nl, mk3(d.x, d.y, d.z)), 0.0f), s.w);  // :163, SpotPower in .w

@@ -4,7 +4,7 @@
 // Every operation is the scalar fast path's operation applied element-wise: a packed instruction
 // rounds each element exactly like its scalar form, so each pixel of the pair gets the bits the
 // scalar fast path (and therefore the compiler's full IEEE sequences) would give it. Transcendental
-// seeds (v_rcp_f32, v_sqrt_f32), compares, selects and the fp64 powf (pow5) have no packed form and run
+// seeds (v_rcp_f32, v_rsq_f32), compares, selects and the fp64 powf (pow5) have no packed form and run
 // per element. Pixels that leave the fast-path window are re-evaluated by the scalar exact path.
 #pragma once
 #include "pbr_device_math.h"
@@ -43,15 +43,11 @@ __device__ __forceinline__ v2 div_nr(v2 x, Recip2 d) {  // Markstein step, see p
     v2 t = vfma(d.y, q, -x);
     return vfma(-t, d.r, q);
 }
-__device__ __forceinline__ v2 sqrt_nr(v2 x) {
-    v2 s = v2{__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
-    v2i si = __builtin_bit_cast(v2i, s);
-    v2 sm = __builtin_bit_cast(v2, si - 1);
-    v2 sp = __builtin_bit_cast(v2, si + 1);
-    v2 rm = vfma(-sm, s, x);
-    v2 rp = vfma(-sp, s, x);
-    s = vsel(rm <= 0.0f, sm, s);
-    return vsel(rp > 0.0f, sp, s);
+__device__ __forceinline__ v2 sqrt_nr(v2 x) {  // see sqrt_nr in pbr_device_math.h
+    const v2 y = v2{__builtin_amdgcn_rsqf(x.x), __builtin_amdgcn_rsqf(x.y)};
+    const v2 s0 = x * y;
+    const v2 r = vfma(-s0, s0, x);
+    return vfma(r, 0.5f * y, s0);
 }
 __device__ __forceinline__ v2 pow5_light(v2 x) { return v2{pow5_light(x.x), pow5_light(x.y)}; }
 // |x| in [lo, hi] per element (false for NaN), as an int mask (-1 / 0).
@@ -111,7 +107,6 @@ __device__ __forceinline__ PixelInvariants unpack_invariants(const PixelInvarian
     s.one_minus_k = i ? q.one_minus_k.y : q.one_minus_k.x;
     s.ggx_v = i ? q.ggx_v.y : q.ggx_v.x;
     s.four_n_dot_v = i ? q.four_n_dot_v.y : q.four_n_dot_v.x;
-    s.r_pi = recip_nr(kPi);
     s.fast_ok = false;
     s.f0_nonzero = (i ? q.f0_nonzero.y : q.f0_nonzero.x) != 0;
     return s;
@@ -119,8 +114,9 @@ __device__ __forceinline__ PixelInvariants unpack_invariants(const PixelInvarian
 
 // BRDFCookTorrance, packed fast path (scalar twin: brdf_cook_torrance<true>). `ok` collects the
 // per-iteration window conditions (see pbr_device_math.h).
-__device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, const Recip2& rpi, f3x2 radiance, f3x2 l, f3x2 h,
-                                        v2i& ok) {
+__device__ __forceinline__ v2 div_pi(v2 x) { return vfma(x, splat(kInvPiHi), x * kInvPiLo); }  // see div_pi
+
+__device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, v2i& ok) {
     v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
     v2 n_dot_h_sqr = n_dot_h * n_dot_h;
     v2 den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
@@ -140,9 +136,9 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, const Recip2&
     const Recip2 rd = recip_nr(denom);
     f3x2 spec = f3x2{div_nr(nom.x, rd), div_nr(nom.y, rd), div_nr(nom.z, rd)};
     f3x2 kd = f3x2{(1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal};
-    return f3x2{((div_nr(kd.x * q.albedo.x, rpi) + spec.x) * radiance.x) * n_dot_l,
-                ((div_nr(kd.y * q.albedo.y, rpi) + spec.y) * radiance.y) * n_dot_l,
-                ((div_nr(kd.z * q.albedo.z, rpi) + spec.z) * radiance.z) * n_dot_l};
+    return f3x2{((div_pi(kd.x * q.albedo.x) + spec.x) * radiance.x) * n_dot_l,
+                ((div_pi(kd.y * q.albedo.y) + spec.y) * radiance.y) * n_dot_l,
+                ((div_pi(kd.z * q.albedo.z) + spec.z) * radiance.z) * n_dot_l};
 }
 
 __device__ __forceinline__ f3x2 normalize_x2(f3x2 v, v2i& ok) {
@@ -153,17 +149,16 @@ __device__ __forceinline__ f3x2 normalize_x2(f3x2 v, v2i& ok) {
 }
 
 // ComputeDirectionalLight, packed fast path.
-__device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, const Recip2& rpi, float4 s, float4 d,
-                                               v2i& ok) {
+__device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, float4 s, float4 d, v2i& ok) {
     f3x2 l = splat3(-d.x, -d.y, -d.z);
     f3x2 h = normalize_x2(add3(q.v, l), ok);
-    return brdf_x2(q, rpi, splat3(s.x, s.y, s.z), l, h, ok);
+    return brdf_x2(q, splat3(s.x, s.y, s.z), l, h, ok);
 }
 
 // ComputePointLight / ComputeSpotLight, packed fast path. `lit` = the range test passed (exact,
 // as in the scalar version). Lanes with lit == 0 carry garbage in `out` and are never added.
 template <bool SPOT>
-__device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const Recip2& rpi, const f3x2& pos,
+__device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const f3x2& pos,
                                                  float4 s, float4 d, float4 p, v2i& lit, v2i& ok) {
     f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
     v2 dist = sqrt_nr(dot3(l, l));
@@ -173,12 +168,12 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     f3x2 h = normalize_x2(add3(q.v, l), ok);
     v2 dsat = vmax(dist, splat(0.01f));
-    v2 att = div_nr(splat(1.0f), recip_nr(dsat * dsat));
+    v2 att = recip_nr(dsat * dsat).r;  // RN(1/y) already (see point_or_spot_light)
     if (SPOT) {
         v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
-    return brdf_x2(q, rpi, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
+    return brdf_x2(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
 }
 
 }  // namespace pbr

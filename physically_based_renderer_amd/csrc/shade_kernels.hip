@@ -126,7 +126,6 @@ template <bool CULL>
 __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, v2i fast_ok,
                                               const float4* __restrict__ lights, const PassArgs& ps, Lds& s,
                                               const TileBounds& tb, bool cull_enabled, v2i& redo, int& kept_total) {
-    const Recip2 rpi = recip_nr(splat(kPi));
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     for (int base = 0; base < ps.n_dir; base += kChunk) {  // directional: never culled
         const int cnt = min(kChunk, ps.n_dir - base);
@@ -136,7 +135,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         for (int j = 0; j < cnt; ++j) {
             const float4* r = &s.light[3 * j];
             v2i ok = fast_ok & (r[2].w != 0.0f ? -1 : 0);
-            const f3x2 c = directional_x2(q, rpi, r[0], r[1], ok);
+            const f3x2 c = directional_x2(q, r[0], r[1], ok);
             redo |= ~ok;
             direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
         }
@@ -158,8 +157,8 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
                 const float4* r = &s.light[3 * j];
                 v2i ok = fast_ok & (r[2].w != 0.0f ? -1 : 0);
                 v2i lit;
-                const f3x2 c = kind == 1 ? point_or_spot_x2<false>(q, rpi, pos, r[0], r[1], r[2], lit, ok)
-                                         : point_or_spot_x2<true>(q, rpi, pos, r[0], r[1], r[2], lit, ok);
+                const f3x2 c = kind == 1 ? point_or_spot_x2<false>(q, pos, r[0], r[1], r[2], lit, ok)
+                                         : point_or_spot_x2<true>(q, pos, r[0], r[1], r[2], lit, ok);
                 redo |= lit & ~ok;
                 // An unlit light adds +0 in the reference (identity on a sum that is never -0).
                 direct = add3(direct, f3x2{vsel(lit, c.x, splat(0.0f)), vsel(lit, c.y, splat(0.0f)),

@@ -68,6 +68,31 @@ __global__ void div_random(uint64_t seed, int iters, int alo, int ahi, int blo, 
     if (nbad_r) atomicAdd(bad_r1, (unsigned long long)nbad_r);
 }
 
+// (3) div_pi (pbr_device_math.h) == x / PI for every significand and exponent in [emin, emax].
+__global__ void div_pi_exhaustive(int emin, int emax, unsigned long long* bad) {
+    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= (1u << 23)) return;
+    const float pi = 3.14159265359f, zh = 0x1.45f306p-2f, zl = 0x1.11be6cp-28f;
+    unsigned int nbad = 0;
+    for (int e = emin; e <= emax; ++e) {
+        const float x = __uint_as_float(((uint32_t)(e + 127) << 23) | m);
+        if (__float_as_uint(__builtin_fmaf(x, zh, x * zl)) != __float_as_uint(x / pi)) ++nbad;
+        if (__float_as_uint(__builtin_fmaf(-x, zh, -x * zl)) != __float_as_uint(-x / pi)) ++nbad;
+    }
+    if (nbad) atomicAdd(bad, (unsigned long long)nbad);
+}
+
+extern "C" int probe_div_pi(int emin, int emax, unsigned long long* bad) {
+    unsigned long long* d_bad;
+    if (hipMalloc(&d_bad, 8) != hipSuccess) return -1;
+    (void)hipMemset(d_bad, 0, 8);
+    hipLaunchKernelGGL(div_pi_exhaustive, dim3((1u << 23) / 256), dim3(256), 0, 0, emin, emax, d_bad);
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    (void)hipMemcpy(bad, d_bad, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    return 0;
+}
+
 extern "C" int probe_recip(int emin, int emax, unsigned long long* bad, unsigned int* first_bad) {
     unsigned long long* d_bad;
     unsigned int* d_first;

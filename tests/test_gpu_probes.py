@@ -26,7 +26,7 @@ FLAGS = ["-O3", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result", "-fPIC"
 def probes(tmp_path_factory, gpu):
     d = tmp_path_factory.mktemp("probes")
     libs = {}
-    for name in ("fastdiv_probe", "libm_probe"):
+    for name in ("fastdiv_probe", "libm_probe", "sqrt_probe"):
         so = str(d / f"{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, os.path.join(ROOT, "tests", "hip", f"{name}.hip"), "-o", so,
                         "-lpthread"], check=True)
@@ -39,6 +39,25 @@ def test_reciprocal_is_correctly_rounded_in_window(probes):
     bad, first = ctypes.c_ulonglong(), ctypes.c_uint()
     assert L.probe_recip(-64, 64, ctypes.byref(bad), ctypes.byref(first)) == 0
     assert bad.value == 0, hex(first.value)
+
+
+def test_rsq_newton_sqrt_is_ieee_in_window(probes):
+    """The fast path's sqrt (v_rsq + one Newton step, pbr_device_math.h sqrt_nr) equals IEEE sqrtf for
+    every float with exponent in [-64, 64]; bare v_sqrt_f32 does not (kept as a control)."""
+    L = probes["sqrt_probe"]
+    bad, first = ctypes.c_ulonglong(), ctypes.c_uint()
+    assert L.probe_sqrt(1, -64, 64, ctypes.byref(bad), ctypes.byref(first)) == 0
+    assert bad.value == 0, hex(first.value)
+    assert L.probe_sqrt(0, -64, 64, ctypes.byref(bad), ctypes.byref(first)) == 0
+    assert bad.value > 0
+
+
+def test_div_pi_is_ieee_on_device(probes):
+    """The fast path's 2-op division by PI over the window's magnitudes [2^-98, 2^100], both signs."""
+    L = probes["fastdiv_probe"]
+    bad = ctypes.c_ulonglong()
+    assert L.probe_div_pi(-98, 100, ctypes.byref(bad)) == 0
+    assert bad.value == 0
 
 
 @pytest.mark.parametrize("alo,ahi,blo,bhi", [(-96, 60, -60, 60), (-30, 30, -30, 30), (-5, 5, -5, 5)])

@@ -245,3 +245,30 @@ def test_reference_scene_fill(camera):
     assert (pc.num_dir_lights, pc.num_point_lights) == (4, 0) and pc.flags & N.PBR_FLAG_F0_PLANE
     L = pc.light_array()
     assert np.allclose(np.abs(L[:, 4:7]), 0.57735) and np.allclose(L[:, 0:3], 0.25)
+
+
+def test_div_pi_is_exact(tmp_path):
+    """pbr_device_math.h div_pi: fma(x, zh, x*zl) == x / 3.14159265359f for every significand (two
+    binades cover every significand and exponent parity; other exponents scale exactly)."""
+    import subprocess
+
+    src = tmp_path / "dp.c"
+    src.write_text(r'''
+#include <math.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <string.h>
+int main(void) {
+    const float pi = 3.14159265359f, zh = 0x1.45f306p-2f, zl = 0x1.11be6cp-28f;
+    if (zh != 1.0f / pi || zl != (float)(1.0 / (double)pi - (double)zh)) { puts("constants"); return 1; }
+    unsigned long long bad = 0;
+    for (uint32_t m = 0; m < (1u << 24); ++m) {
+        uint32_t u = 0x3f800000u + m; float x; memcpy(&x, &u, 4);
+        if (fmaf(x, zh, x * zl) != x / pi) ++bad;
+    }
+    printf("%llu\n", bad);
+    return 0;
+}''')
+    exe = str(tmp_path / "dp")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", str(src), "-o", exe, "-lm"], check=True)
+    assert subprocess.run([exe], capture_output=True, text=True, check=True).stdout.strip() == "0"
