@@ -2,6 +2,7 @@
 // the shade entry point. Host code only; the kernels live in shade_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -189,6 +190,11 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
         p.fresnel_r0[i] = pass->fresnel_r0[i];
     }
     p.opacity = pass->opacity;
+    p.eye_ok = 1;
+    for (int i = 0; i < 3; ++i) {  // the fast-path window of the (uniform) eye: 0 or |x| in [2^-20, 2^20]
+        const float a = std::fabs(pass->eye_pos_w[i]);
+        if (!(a == 0.0f || (a >= 0x1p-20f && a <= 0x1p20f))) p.eye_ok = 0;
+    }
     p.n_dir = nd;
     p.n_point = np;
     p.n_spot = ns;

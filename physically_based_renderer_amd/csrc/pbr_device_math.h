@@ -46,8 +46,6 @@ __device__ __forceinline__ float hlerp(float x, float y, float s) { return x + s
 // Window (proved per pixel-light by the callers, see fast_window_ok): 0 < b in [2^-60, 2^60];
 // a == +-0 or |a| in [2^-96, 2^60]; |a / b| in [2^-120, 2^120] (no overflow, no subnormal q0 or t).
 // One reciprocal serves every numerator with the same denominator (L/d, normalize, specular, /PI).
-// sqrt_nr replicates hipcc's correctly rounded sqrt (v_sqrt + a +-1 ulp correction) without its
-// scaling and class fix-up, exact for x in [2^-96, 2^128).
 // The light loop falls back to the compiler's full sequences whenever the window is not proved;
 // PBR_FLAG_EXACT_ONLY runs only those, and tests require both modes to agree bit for bit
 // (tests/test_gpu_parity.py::test_fast_path_is_bit_identical_to_exact_only).
@@ -156,17 +154,30 @@ struct PixelInvariants {
 //   in [0.125, 48.5]; kD*albedo is 0 or in [2^-68, 2^21].
 // Together with the per-iteration compares in the light functions this keeps every fast-path
 // division and sqrt inside the windows stated above.
-__device__ __forceinline__ bool fast_window_ok(f3 pos, f3 eye, f3 n, f3 albedo, f3 f0, float metallic,
-                                               float roughness) {
-    const float lo = 0x1p-20f;
-    bool ok = zero_or_in(pos.x, lo, 0x1p20f) && zero_or_in(pos.y, lo, 0x1p20f) && zero_or_in(pos.z, lo, 0x1p20f);
-    ok = ok && zero_or_in(eye.x, lo, 0x1p20f) && zero_or_in(eye.y, lo, 0x1p20f) && zero_or_in(eye.z, lo, 0x1p20f);
-    ok = ok && zero_or_in(n.x, lo, 16.0f) && zero_or_in(n.y, lo, 16.0f) && zero_or_in(n.z, lo, 16.0f);
-    ok = ok && zero_or_in(albedo.x, lo, 1024.0f) && zero_or_in(albedo.y, lo, 1024.0f) &&
-         zero_or_in(albedo.z, lo, 1024.0f);
-    ok = ok && zero_or_in(f0.x, lo, 1024.0f) && zero_or_in(f0.y, lo, 1024.0f) && zero_or_in(f0.z, lo, 1024.0f);
-    ok = ok && metallic >= 0.0f && metallic <= 1.0f && roughness >= 0.0f && roughness <= 1.0f;
-    return ok;
+// The per-pixel window as unsigned min/max over bit patterns (no compare-and-branch chains): a value
+// passes "0 or |x| in [2^-20, hi]" iff b = bits(|x|) satisfies b - 1 >= bits(2^-20) - 1 (unsigned:
+// b = 0 wraps to the maximum) and b <= bits(hi); NaN and inf exceed every hi. Metallic and roughness
+// must lie in [0, 1] (or be -0). The eye position (uniform) is checked once on the host (PassArgs).
+__device__ __forceinline__ uint32_t abs_bits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) { return min(min(a, b), c); }
+__device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) { return max(max(a, b), c); }
+__device__ __forceinline__ bool unit_or_neg_zero(float x) {
+    const uint32_t b = __float_as_uint(x);
+    return b <= 0x3f800000u || b == 0x80000000u;
+}
+__device__ __forceinline__ bool fast_window_ok(f3 pos, f3 n, f3 albedo, f3 f0, float metallic, float roughness) {
+    const uint32_t bp[3] = {abs_bits(pos.x), abs_bits(pos.y), abs_bits(pos.z)};
+    const uint32_t bn[3] = {abs_bits(n.x), abs_bits(n.y), abs_bits(n.z)};
+    const uint32_t ba[3] = {abs_bits(albedo.x), abs_bits(albedo.y), abs_bits(albedo.z)};
+    const uint32_t bf[3] = {abs_bits(f0.x), abs_bits(f0.y), abs_bits(f0.z)};
+    const uint32_t lo = umin3(umin3(bp[0] - 1u, bp[1] - 1u, bp[2] - 1u), umin3(bn[0] - 1u, bn[1] - 1u, bn[2] - 1u),
+                              min(umin3(ba[0] - 1u, ba[1] - 1u, ba[2] - 1u), umin3(bf[0] - 1u, bf[1] - 1u, bf[2] - 1u)));
+    const bool lo_ok = lo >= 0x35800000u - 1u;                          // 2^-20
+    const bool pos_ok = umax3(bp[0], bp[1], bp[2]) <= 0x49800000u;      // 2^20
+    const bool n_ok = umax3(bn[0], bn[1], bn[2]) <= 0x41800000u;        // 16
+    const bool af_ok = max(umax3(ba[0], ba[1], ba[2]), umax3(bf[0], bf[1], bf[2])) <= 0x44800000u;  // 1024
+    return ((int)lo_ok & (int)pos_ok & (int)n_ok & (int)af_ok & (int)unit_or_neg_zero(metallic) &
+            (int)unit_or_neg_zero(roughness)) != 0;
 }
 
 // F0 with no zero component: then F = F0 + (1-F0) p stays >= 2^-20 for any p (see brdf checks).
@@ -317,8 +328,13 @@ __device__ __forceinline__ void world_to_sky_uv(f3 c, float& u, float& v) {
 
 __device__ __forceinline__ int wrap_index(float f, int n) {
     if (!(f == f) || f > 2.0e9f || f < -2.0e9f) return 0;  // NaN coordinate: the weights are NaN anyway
-    int i = (int)f % n;
-    return i < 0 ? i + n : i;
+    const int i = (int)f;
+    if (__builtin_expect(i >= -n && i < 2 * n, 1)) {  // every finite WorldToSkyUV texel: one wrap at most
+        const int j = i < 0 ? i + n : i;
+        return j >= n ? j - n : j;                     // == ((i % n) + n) % n on this range
+    }
+    const int m = i % n;
+    return m < 0 ? m + n : m;
 }
 
 // Linear-wrap bilinear sample (g_SamLinearWrap, PBRApp.cpp:1157-1162) of the fp32 RGBA env map

@@ -62,9 +62,12 @@ struct PixelInvariants2 {
     v2i f0_nonzero;  // -1 where no F0 component is zero
 };
 
-// make_invariants (pbr_device_math.h) element-wise for the pair: the same operations, packed.
+// make_invariants (pbr_device_math.h) element-wise for the pair: the same operations, packed. The one
+// division, GeometrySchlickGGX(N.V) = n_dot_v / (n_dot_v (1-k) + k), takes the Markstein step for
+// pixels in the fast window (`fast`): roughness in [0, 1] puts k in [1/8, 1/2] and the denominator in
+// [2^-3, 2^5]; n_dot_v must be 0 or >= 2^-100 so the residual stays normal. Otherwise IEEE.
 __device__ __forceinline__ PixelInvariants2 make_invariants(const f3x2& n, const f3x2& v, const f3x2& albedo,
-                                                            const f3x2& f0, v2 metallic, v2 roughness) {
+                                                            const f3x2& f0, v2 metallic, v2 roughness, v2i fast) {
     PixelInvariants2 q;
     q.n = n;
     q.v = v;
@@ -80,7 +83,14 @@ __device__ __forceinline__ PixelInvariants2 make_invariants(const f3x2& n, const
     q.k = (rr * rr) * 0.125f;  // (r*r) / 8.0f: division by a power of two is this exact product
     q.one_minus_k = 1.0f - q.k;
     v2 n_dot_v = vmax(dot3(n, v), splat(0.0f));
-    q.ggx_v = n_dot_v / (n_dot_v * q.one_minus_k + q.k);  // IEEE division per element
+    const v2 den = n_dot_v * q.one_minus_k + q.k;
+    const v2i ok = fast & ((n_dot_v == 0.0f) | (n_dot_v >= 0x1p-100f));
+    const v2 gq = div_nr(n_dot_v, recip_nr(den));
+    if (__builtin_expect(ok.x & ok.y, 1)) {
+        q.ggx_v = gq;
+    } else {
+        q.ggx_v = v2{ok.x ? gq.x : n_dot_v.x / den.x, ok.y ? gq.y : n_dot_v.y / den.y};
+    }
     q.four_n_dot_v = 4.0f * n_dot_v;
     q.f0_nonzero = (f0.x != 0.0f) & (f0.y != 0.0f) & (f0.z != 0.0f);
     return q;

@@ -27,6 +27,7 @@ struct PassArgs {
     int n_dir, n_point, n_spot;
     int env_w, env_h;
     int sky_w, sky_h;
+    int eye_ok;  // the eye position is inside the fast-path window (0 or |x| in [2^-20, 2^20]), host-checked
 };
 
 constexpr int kOutRgba32f = 0;

@@ -259,9 +259,16 @@ __device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArg
 }
 
 // Ambient + tonemap + gamma for one pixel (Default.hlsl:139-160), returns the output RGBA.
+// Reinhard c / (c + 1) (Default.hlsl:153, Skybox.hlsl:47): the Markstein step when `fast` and c is 0 or
+// in [2^-100, 2^60] (then c + 1 is in [1, 2^60]); the IEEE division otherwise.
+__device__ __forceinline__ float reinhard(float c, bool fast) {
+    if (fast && (c == 0.0f || (c >= 0x1p-100f && c <= 0x1p60f))) return div_nr(c, recip_nr(c + 1.0f));
+    return c / (c + 1.0f);
+}
+
 template <int AMBIENT, bool APPLY_AO>
 __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float ao, f3 direct, const PassArgs& ps,
-                                               const float4* __restrict__ env) {
+                                               const float4* __restrict__ env, bool fast) {
     const PixelInvariants& q = p;
     f3 ambient;
     if (AMBIENT == kAmbientIblDiffuse) {
@@ -283,19 +290,19 @@ __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float a
     }
     if (APPLY_AO) ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
     f3 lit = add3(ambient, direct);
-    lit = mk3(lit.x / (lit.x + 1.0f), lit.y / (lit.y + 1.0f), lit.z / (lit.z + 1.0f));  // Default.hlsl:153
+    lit = mk3(reinhard(lit.x, fast), reinhard(lit.y, fast), reinhard(lit.z, fast));  // Default.hlsl:153
     return make_float4(powf_glibc(lit.x, kInvGamma), powf_glibc(lit.y, kInvGamma), powf_glibc(lit.z, kInvGamma),
                        ps.opacity);
 }
 
 // The sky pass for a background pixel (Skybox.hlsl:37-49): sampleCoord = normalize(PosW);
 // WorldToSkyUV; g_SkyArray[0].Sample(linear-wrap); Reinhard; gamma; alpha 1.
-__device__ __forceinline__ float4 sky_pixel(f3 dir, const PassArgs& ps, const float4* __restrict__ sky) {
+__device__ __forceinline__ float4 sky_pixel(f3 dir, const PassArgs& ps, const float4* __restrict__ sky, bool fast) {
     const f3 c = normalize3(dir);
     float u, v;
     world_to_sky_uv(c, u, v);
     f3 col = sample_linear_wrap(sky, ps.sky_w, ps.sky_h, u, v);
-    col = mk3(col.x / (col.x + 1.0f), col.y / (col.y + 1.0f), col.z / (col.z + 1.0f));
+    col = mk3(reinhard(col.x, fast), reinhard(col.y, fast), reinhard(col.z, fast));
     return make_float4(powf_glibc(col.x, kInvGamma), powf_glibc(col.y, kInvGamma), powf_glibc(col.z, kInvGamma),
                        1.0f);
 }
@@ -349,14 +356,23 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                    vb && gb.pairs_aligned);
     const f3 pa = lane(p.pos, 0), pb = lane(p.pos, 1);
 
-    // V = normalize(g_CameraPosW - pin.PosW)  (Default.hlsl:53)
-    const f3 eye = mk3(ps.eye[0], ps.eye[1], ps.eye[2]);
-    const f3x2 v = normalize_ieee(f3x2{ps.eye[0] - p.pos.x, ps.eye[1] - p.pos.y, ps.eye[2] - p.pos.z});
-    const PixelInvariants2 q2 = make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness);
-    const bool ok_a = !exact_only && fast_window_ok(pa, eye, lane(p.n, 0), lane(p.albedo, 0), lane(p.f0, 0),
+    const bool ok_a = !exact_only && ps.eye_ok && fast_window_ok(pa, lane(p.n, 0), lane(p.albedo, 0), lane(p.f0, 0),
                                                     p.metallic.x, p.roughness.x);
-    const bool ok_b = !exact_only && fast_window_ok(pb, eye, lane(p.n, 1), lane(p.albedo, 1), lane(p.f0, 1),
+    const bool ok_b = !exact_only && ps.eye_ok && fast_window_ok(pb, lane(p.n, 1), lane(p.albedo, 1), lane(p.f0, 1),
                                                     p.metallic.y, p.roughness.y);
+    const v2i fast2 = v2i{ok_a ? -1 : 0, ok_b ? -1 : 0};
+
+    // V = normalize(g_CameraPosW - pin.PosW)  (Default.hlsl:53). In the window every component of
+    // eye - pos is 0 or >= 2^-44 and |eye - pos| < 2^22, so the exact fast normalize applies once
+    // |V| >= 2^-30; other pixels take the IEEE sequences.
+    const f3x2 ve = f3x2{ps.eye[0] - p.pos.x, ps.eye[1] - p.pos.y, ps.eye[2] - p.pos.z};
+    v2i okv = fast2;
+    f3x2 v = normalize_x2(ve, okv);
+    if (__builtin_expect(!(okv.x & okv.y), 0)) {
+        const f3 v0 = okv.x ? lane(v, 0) : normalize3(lane(ve, 0)), v1 = okv.y ? lane(v, 1) : normalize3(lane(ve, 1));
+        v = f3x2{v2{v0.x, v1.x}, v2{v0.y, v1.y}, v2{v0.z, v1.z}};
+    }
+    const PixelInvariants2 q2 = make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness, fast2);
 
     TileBounds tb{};
     bool cull_enabled = false;
@@ -417,8 +433,12 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     }
 
     const int64_t orow = (int64_t)y * fr.out_stride;
-    if (va) store_pixel(fr, orow + xa, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env) : sky_pixel(ua.n, ps, fr.sky));
-    if (vb) store_pixel(fr, orow + xa + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env) : sky_pixel(ub.n, ps, fr.sky));
+    if (va)
+        store_pixel(fr, orow + xa, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a)
+                                      : sky_pixel(ua.n, ps, fr.sky, !exact_only));
+    if (vb)
+        store_pixel(fr, orow + xa + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b)
+                                           : sky_pixel(ub.n, ps, fr.sky, !exact_only));
 }
 
 // ---- One pixel per work-item (32x8 tiles) ---------------------------------------------------------
@@ -509,7 +529,7 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
     // V = normalize(g_CameraPosW - pin.PosW)  (Default.hlsl:53)
     const f3 eye = mk3(ps.eye[0], ps.eye[1], ps.eye[2]);
     PixelInvariants q = make_invariants(n, normalize3(sub3(eye, pos)), albedo, f0, metallic, roughness);
-    q.fast_ok = !exact_only && fast_window_ok(pos, eye, n, albedo, f0, metallic, roughness);
+    q.fast_ok = !exact_only && ps.eye_ok && fast_window_ok(pos, n, albedo, f0, metallic, roughness);
 
     TileBounds tb{};
     bool cull_enabled = false;
@@ -550,7 +570,8 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
     }
     if (valid)
         store_pixel(fr, (int64_t)y * fr.out_stride + x,
-                    geom ? finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env) : sky_pixel(q.n, ps, fr.sky));
+                    geom ? finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env, q.fast_ok)
+                         : sky_pixel(q.n, ps, fr.sky, !exact_only));
 }
 
 __global__ void decode_unorm16_kernel(const uint16_t* __restrict__ src, float4* __restrict__ dst, int n) {
