@@ -103,9 +103,13 @@ __device__ __forceinline__ void load_libm_tables() {
     if (t >= 32 && t < 64) g_lds_exp2f[t - 32] = pbr_exp2f_tab[t - 32];
 }
 #define PBR_POW5_TABLES g_lds_powf_log2, g_lds_exp2f
+#define PBR_LIBM_LOG2_TAB g_lds_powf_log2
+#define PBR_LIBM_EXP2_TAB g_lds_exp2f
 #else
 __device__ __forceinline__ void load_libm_tables() {}
 #define PBR_POW5_TABLES pbr_powf_log2_tab, pbr_exp2f_tab
+#define PBR_LIBM_LOG2_TAB pbr_powf_log2_tab
+#define PBR_LIBM_EXP2_TAB pbr_exp2f_tab
 #endif
 #ifndef PBR_POW5_GLIBC_FROM  // x above which pow5_light switches to glibc's algorithm
 #define PBR_POW5_GLIBC_FROM 0.99f
@@ -130,6 +134,17 @@ constexpr float kPi = 3.14159265359f;  // LightingUtil.hlsl:59, 103 (an fp32 lit
 constexpr float kInvPiHi = 0x1.45f306p-2f, kInvPiLo = 0x1.11be6cp-28f;
 __device__ __forceinline__ float div_pi(float x) { return __builtin_fmaf(x, kInvPiHi, x * kInvPiLo); }
 constexpr float kInvGamma = 1.0f / 2.2f;  // Default.hlsl:155
+
+// pow(c, 1/2.2) of the gamma step (Default.hlsl:155, Skybox.hlsl:48) as glibc's powf: for c in
+// [2^-126, 1) -- every tonemapped value of a finite non-negative colour but 0 -- none of powf's special
+// cases apply and |y log2 c| < 58 cannot overflow, so its main path runs directly on the LDS tables;
+// anything else takes the general function.
+__device__ __forceinline__ float pow_inv_gamma(float c) {
+    const uint32_t ix = __float_as_uint(c);
+    if (__builtin_expect(ix - 0x00800000u < 0x3f800000u - 0x00800000u, 1))
+        return pbr_powf_exp2((double)kInvGamma * pbr_powf_log2(ix, PBR_LIBM_LOG2_TAB), 0u, PBR_LIBM_EXP2_TAB);
+    return pbr_powf(c, kInvGamma);
+}
 constexpr float kLightRange = 100.0f;     // LightingUtil.hlsl:131
 
 // Everything BRDFCookTorrance (LightingUtil.hlsl:85-104) needs that does not depend on the light.

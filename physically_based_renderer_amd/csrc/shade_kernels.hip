@@ -291,7 +291,7 @@ __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float a
     if (APPLY_AO) ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
     f3 lit = add3(ambient, direct);
     lit = mk3(reinhard(lit.x, fast), reinhard(lit.y, fast), reinhard(lit.z, fast));  // Default.hlsl:153
-    return make_float4(powf_glibc(lit.x, kInvGamma), powf_glibc(lit.y, kInvGamma), powf_glibc(lit.z, kInvGamma),
+    return make_float4(pow_inv_gamma(lit.x), pow_inv_gamma(lit.y), pow_inv_gamma(lit.z),
                        ps.opacity);
 }
 
@@ -303,7 +303,7 @@ __device__ __forceinline__ float4 sky_pixel(f3 dir, const PassArgs& ps, const fl
     world_to_sky_uv(c, u, v);
     f3 col = sample_linear_wrap(sky, ps.sky_w, ps.sky_h, u, v);
     col = mk3(reinhard(col.x, fast), reinhard(col.y, fast), reinhard(col.z, fast));
-    return make_float4(powf_glibc(col.x, kInvGamma), powf_glibc(col.y, kInvGamma), powf_glibc(col.z, kInvGamma),
+    return make_float4(pow_inv_gamma(col.x), pow_inv_gamma(col.y), pow_inv_gamma(col.z),
                        1.0f);
 }
 
