@@ -188,3 +188,37 @@ def test_reference_scene_frame(camera, shading_ctx, gpu):
         ref = O.shade_frame(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, sky, cov,
                             O.OUTPUT_RGBA8 if fmt == N.PBR_OUTPUT_RGBA8_UNORM else O.OUTPUT_RGBA32F, n_threads=8)
         check(got, ref, cov, fmt, f"reference scene camera={camera} fmt={fmt}")
+
+
+def test_one_pixel_layout_matches_pair_layout(gpu, env_map):
+    """The 1-pixel-per-work-item kernel (PBR_PIXELS_PER_THREAD=1, 32x8 tiles) is bit-identical to the
+    default pixel-pair kernel: plain, culled, with background pixels and RGBA8 output, and under
+    EXACT_ONLY."""
+    from physically_based_renderer_amd.renderer import ShadingContext
+
+    cfg = S.CONFIGS[4].with_size(300, 40)  # partial tiles in both layouts
+    planes, _ = S.fill_gbuffer_host(cfg)
+    rng = np.random.default_rng(11)
+    cov = (rng.uniform(size=(40, 300)) > 0.2).astype(np.uint8)
+    sky = envmap.procedural_sky_rgba16(64, 32)
+    pc = S.scene_pass(cfg)
+    old = os.environ.get("PBR_PIXELS_PER_THREAD")
+    try:
+        results = []
+        for layout in ("2", "1"):
+            os.environ["PBR_PIXELS_PER_THREAD"] = layout
+            ctx = ShadingContext(0)
+            outs = []
+            for flags in (pc.flags, pc.flags & ~N.PBR_FLAG_TILED_CULLING, pc.flags | N.PBR_FLAG_EXACT_ONLY):
+                p2 = PassConstants(**{**pc.__dict__, "flags": flags, "ambient_mode": N.PBR_AMBIENT_IBL_DIFFUSE})
+                for fmt in (N.PBR_OUTPUT_RGBA32F, N.PBR_OUTPUT_RGBA8_UNORM):
+                    outs.append(run_frame(ctx, gpu, planes, p2, env_map, sky, cov, fmt))
+            ctx.close()
+            results.append(outs)
+        for a, b in zip(*results):
+            assert (np.array_equal(a, b) if a.dtype == np.uint8 else O.bit_equal(a, b).all())
+    finally:
+        if old is None:
+            os.environ.pop("PBR_PIXELS_PER_THREAD", None)
+        else:
+            os.environ["PBR_PIXELS_PER_THREAD"] = old
