@@ -40,6 +40,7 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, vector FP32 (spec)
 # Algorithmic FLOP per pixel (+,-,*,/,sqrt,pow = 1 each after parity-safe hoisting):
 # base 27 + 20 hoisted BRDF invariants + 91 per point light + 87 for the diffuse IBL.
 FLOP_BASE, FLOP_HOIST, FLOP_POINT, FLOP_IBL = 27, 20, 91, 87
+FLOP_RANGE_TEST = 9  # per light and tile under tiled culling (box distance + compare)
 
 
 def log(*a):
@@ -57,12 +58,20 @@ def bytes_per_pixel(pc, out_bytes: int = 16) -> int:
     return planes * 4 + out_bytes
 
 
-def flops_per_pixel(pc) -> int:
-    f = FLOP_BASE + FLOP_HOIST + FLOP_POINT * (pc.num_point_lights + pc.num_spot_lights)
+def flops_per_pixel(pc, lights_per_tile=None, tile_px: int = 512) -> float:
+    """Algorithmic FLOP per pixel. With tiled culling only the lights that survive a tile are shaded
+    (base + L_in per-light BRDFs); the 9-FLOP range test of every point/spot light is
+    counted once per tile (the unit that runs it), not per pixel, so skipped work is never counted."""
+    n_ps = pc.num_point_lights + pc.num_spot_lights
+    f = FLOP_BASE + FLOP_HOIST
+    if pc.flags & N.PBR_FLAG_TILED_CULLING and lights_per_tile is not None:
+        f += FLOP_POINT * lights_per_tile + FLOP_RANGE_TEST * n_ps / tile_px
+    else:
+        f += FLOP_POINT * n_ps
     f += (FLOP_POINT - 17) * pc.num_dir_lights  # 74 per directional light (no distance/attenuation)
     if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE:
         f += FLOP_IBL
-    return f
+    return round(f, 2)
 
 
 def load_pmc(workload: str):
@@ -261,7 +270,8 @@ def main():
         bpp = bytes_per_pixel(pc, 4 if rgba8 else 16)
         achieved = bpp * band_px / avg_kernel_s / 1e9
         traffic, valu_busy = load_pmc(workload)
-        fpp = flops_per_pixel(pc)
+        tile_px = 256 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 512  # 32x8 or 64x8 tiles
+        fpp = flops_per_pixel(pc, cull_note.get("lights_per_tile"), tile_px)
         tflops = fpp * band_px / avg_kernel_s / 1e12
         # At 64 lights the arithmetic intensity (fpp / bpp ~ 99 FLOP/B) is 5x the ridge point, so the
         # compute roof bounds the kernel: FP32 at 157.3 TF (MI355X_MICROARCH.md: the FP32 vector rate,

@@ -160,7 +160,8 @@ int pbr_set_sky_map_f32(pbr_context* ctx, const float* texels, int32_t width, in
 int pbr_shade_frame(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* frame, void* stream);
 
 /* Tiled-culling statistics of the last culled pass on `stream` (synchronises that stream):
- * total surviving point/spot lights summed over tiles, and the tile count. */
+ * total surviving point/spot lights summed over the tiles that hold geometry, and the number of those
+ * tiles. The kernel writes one count per tile (no atomics); this call sums them on the host. */
 int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream);
 
 /* ---- Host G-buffer fill (replaces the VS + rasteriser front-end, Default.hlsl:22-45) ---------- */

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <vector>
 #include <new>
 #include <string>
 
@@ -37,7 +38,11 @@ struct pbr_context {
     int ambient_mode = 0;
     uint32_t flags = 0;
     bool pass_set = false;
-    unsigned long long* d_cull_stats = nullptr;
+    // Tiled-culling statistics of the last culled pass: one int32 per tile (surviving lights, -1 = no
+    // geometry), summed on the host by pbr_last_cull_stats.
+    int32_t* d_tile_kept = nullptr;
+    int64_t tile_kept_capacity = 0;
+    int64_t last_cull_tiles = 0;
     int pixels_per_thread = 2;  // kernel layout: packed pixel pairs (measured faster); PBR_PIXELS_PER_THREAD=1 overrides
     std::string last_error;
     std::mutex mu;
@@ -103,8 +108,7 @@ int pbr_context_create(int device, pbr_context** out_ctx) {
         delete ctx;
         return PBR_ERR_NO_DEVICE;
     }
-    hipError_t e = hipMalloc(&ctx->d_cull_stats, 2 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(ctx->d_cull_stats, 0, 2 * sizeof(unsigned long long));
+    hipError_t e = hipSuccess;
     for (int i = 0; e == hipSuccess && i < pbr_context::kRing; ++i) {
         e = hipHostMalloc(reinterpret_cast<void**>(&ctx->h_ring[i]), sizeof(pbr_light) * PBR_MAX_LIGHTS,
                           hipHostMallocDefault);
@@ -132,7 +136,7 @@ int pbr_context_destroy(pbr_context* ctx) {
             if (t->d_u16) (void)hipFree(t->d_u16);
             if (t->d) (void)hipFree(t->d);
         }
-        if (ctx->d_cull_stats) (void)hipFree(ctx->d_cull_stats);
+        if (ctx->d_tile_kept) (void)hipFree(ctx->d_tile_kept);
     }
     delete ctx;
     return PBR_OK;
@@ -297,7 +301,6 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     a.frame.coverage = fr->coverage;
     a.frame.coverage_stride = fr->coverage_row_stride;
     a.frame.sky = ctx->sky.d;
-    a.cull_stats = ctx->d_cull_stats;
     a.ambient_mode = ctx->ambient_mode;
     a.f0_plane = f0_plane;
     a.apply_ao = apply_ao;
@@ -310,8 +313,23 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     if (cull) {
-        e = hipMemsetAsync(ctx->d_cull_stats, 0, 2 * sizeof(unsigned long long), s);
-        if (e != hipSuccess) return fail_hip(ctx, e, "cull stats reset");
+        const int64_t tiles = pbr::shade_tile_count(gb->width, gb->height, a.pixels_per_thread);
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (tiles > ctx->tile_kept_capacity) {
+            // Growing: the old buffer may still be written by queued kernels on any stream.
+            if (ctx->d_tile_kept) {
+                e = hipDeviceSynchronize();
+                if (e != hipSuccess) return fail_hip(ctx, e, "cull stats sync");
+                (void)hipFree(ctx->d_tile_kept);
+                ctx->d_tile_kept = nullptr;
+                ctx->tile_kept_capacity = 0;
+            }
+            e = hipMalloc(&ctx->d_tile_kept, sizeof(int32_t) * (size_t)tiles);
+            if (e != hipSuccess) return fail_hip(ctx, e, "cull stats hipMalloc");
+            ctx->tile_kept_capacity = tiles;
+        }
+        ctx->last_cull_tiles = tiles;
+        a.tile_kept = ctx->d_tile_kept;
     }
     e = pbr::launch_shade(a, s);
     if (e != hipSuccess) return fail_hip(ctx, e, "shade_tile_kernel launch", PBR_ERR_LAUNCH);
@@ -359,13 +377,20 @@ int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num
     if (!ctx || !sum_tile_lights || !num_tiles) return PBR_ERR_INVALID_ARGUMENT;
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;
-    unsigned long long h[2] = {0, 0};
+    *sum_tile_lights = 0;
+    *num_tiles = 0;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->last_cull_tiles == 0) return PBR_OK;  // no culled pass yet
+    std::vector<int32_t> h((size_t)ctx->last_cull_tiles);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipError_t e = hipMemcpyAsync(h, ctx->d_cull_stats, sizeof(h), hipMemcpyDeviceToHost, s);
+    hipError_t e = hipMemcpyAsync(h.data(), ctx->d_tile_kept, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail_hip(ctx, e, "pbr_last_cull_stats");
-    *sum_tile_lights = (int64_t)h[0];
-    *num_tiles = (int64_t)h[1];
+    for (int32_t k : h) {
+        if (k < 0) continue;  // tile without geometry (sky only): not shaded, not counted
+        *sum_tile_lights += k;
+        *num_tiles += 1;
+    }
     return PBR_OK;
 }
 

@@ -49,7 +49,10 @@ struct LaunchArgs {
     const float4* lights;  // 3 float4 per light (the reference's 48-byte Light)
     const float4* env;     // env_w * env_h RGBA fp32, or nullptr
     FrameArgs frame;
-    unsigned long long* cull_stats;  // [sum kept lights, tiles], CULL only
+    // CULL only: one slot per tile (blockIdx.y * gridDim.x + blockIdx.x) receives the tile's surviving
+    // point/spot light count, or -1 for a tile with no geometry (plain stores: one same-address atomic
+    // per tile serialised the whole grid, 0.29 ms per 4K frame).
+    int32_t* tile_kept;
     int ambient_mode;
     bool f0_plane, apply_ao, cull;
     bool exact_only;  // PBR_FLAG_EXACT_ONLY: skip the exact fast path (validation mode)
@@ -57,6 +60,8 @@ struct LaunchArgs {
 };
 
 hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);
+// Number of tiles (workgroups) launch_shade uses for a width x height G-buffer.
+int64_t shade_tile_count(int width, int height, int pixels_per_thread);
 hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream);
 
 }  // namespace pbr

@@ -335,7 +335,7 @@ template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GBufferArgs gb, PassArgs ps,
                                                             const float4* __restrict__ lights,
                                                             const float4* __restrict__ env, FrameArgs fr,
-                                                            unsigned long long* __restrict__ cull_stats,
+                                                            int32_t* __restrict__ tile_kept,
                                                             bool exact_only) {
     __shared__ Lds s;
     load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
@@ -427,10 +427,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         if (need_a) da = ea;
         if (need_b) db = eb;
     }
-    if (CULL && tid == 0 && cull_stats != nullptr && any_geometry) {
-        atomicAdd(&cull_stats[0], (unsigned long long)kept_total);
-        atomicAdd(&cull_stats[1], 1ull);
-    }
+    if (CULL && tid == 0 && tile_kept != nullptr)
+        tile_kept[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = any_geometry ? kept_total : -1;
 
     const int64_t orow = (int64_t)y * fr.out_stride;
     if (va)
@@ -500,7 +498,7 @@ template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, PassArgs ps,
                                                              const float4* __restrict__ lights,
                                                              const float4* __restrict__ env, FrameArgs fr,
-                                                             unsigned long long* __restrict__ cull_stats,
+                                                             int32_t* __restrict__ tile_kept,
                                                              bool exact_only) {
     __shared__ Lds s;
     load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
@@ -564,10 +562,8 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
         lighting_exact<CULL>(q, q, pos, pos, need, false, lights, ps, s, tb, cull_enabled, e, unused);
         if (need) direct = e;
     }
-    if (CULL && tid == 0 && cull_stats != nullptr && any_geometry) {
-        atomicAdd(&cull_stats[0], (unsigned long long)kept_total);
-        atomicAdd(&cull_stats[1], 1ull);
-    }
+    if (CULL && tid == 0 && tile_kept != nullptr)
+        tile_kept[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = any_geometry ? kept_total : -1;
     if (valid)
         store_pixel(fr, (int64_t)y * fr.out_stride + x,
                     geom ? finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env, q.fast_ok)
@@ -588,11 +584,11 @@ static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
     if (a.pixels_per_thread == 2) {
         dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
         hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream, a.gb,
-                           a.ps, a.lights, a.env, a.frame, a.cull_stats, a.exact_only);
+                           a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
     } else {
         dim3 grid((a.gb.width + kTileW1 - 1) / kTileW1, (a.gb.height + kTileH - 1) / kTileH);
         hipLaunchKernelGGL((shade_tile1_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,
-                           a.gb, a.ps, a.lights, a.env, a.frame, a.cull_stats, a.exact_only);
+                           a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
     }
     return hipGetLastError();
 }
@@ -615,6 +611,11 @@ hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream) {
     if (a.gb.width <= 0 || a.gb.height <= 0) return hipSuccess;
     return a.ambient_mode == kAmbientIblDiffuse ? dispatch_f0<kAmbientIblDiffuse>(a, stream)
                                                 : dispatch_f0<kAmbientConstant>(a, stream);
+}
+
+int64_t shade_tile_count(int width, int height, int pixels_per_thread) {
+    const int tw = pixels_per_thread == 2 ? kTileW : kTileW1;
+    return (int64_t)((width + tw - 1) / tw) * ((height + kTileH - 1) / kTileH);
 }
 
 hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream) {
