@@ -100,6 +100,58 @@ def test_tiled_culling_is_bit_exact(shading_ctx, gpu):
     assert 0 < mean_kept < cfg.n_lights / 4
 
 
+def host_tile_survivors(planes, lights, tile_w, tile_h=8):
+    """The kernel's per-tile range test (shade_kernels.hip, stage_chunk) emulated in float32: box
+    distance per axis with maxNum, (dx*dx + dy*dy) + dz*dz rounded per operation, <= 100.01f^2."""
+    h, w = planes.shape[1:]
+    th, tw = -(-h // tile_h), -(-w // tile_w)
+    pad = np.full((3, th * tile_h, tw * tile_w), np.nan, np.float32)
+    pad[:, :h, :w] = planes[0:3]
+    t = pad.reshape(3, th, tile_h, tw, tile_w)
+    lo = np.nanmin(t, axis=(2, 4)).reshape(3, -1)
+    hi = np.nanmax(t, axis=(2, 4)).reshape(3, -1)
+    r2 = np.float32(100.01) * np.float32(100.01)
+    total = 0
+    for lp in lights[:, 8:11].astype(np.float32):
+        d = [np.maximum(np.maximum(lo[i] - lp[i], lp[i] - hi[i]), np.float32(0)) for i in range(3)]
+        total += int(((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2] <= r2).sum())
+    return total, th * tw
+
+
+def test_cull_stats_equal_host_emulation(shading_ctx, gpu):
+    """pbr_last_cull_stats (one count per tile, summed on the host) equals the range test emulated on
+    the host, at the full config-4 size and on a ragged frame."""
+    tile_w = 32 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 64
+    for cfg in (S.CONFIGS[4], S.CONFIGS[4].with_size(1000, 203)):
+        planes, _ = S.fill_gbuffer_host(cfg)
+        pc = S.scene_pass(cfg)
+        shading_ctx.set_pass(pc)
+        shading_ctx.shade(GBuffer.from_host(planes, gpu))
+        kept, tiles = shading_ctx.cull_stats()
+        want_kept, want_tiles = host_tile_survivors(planes, pc.light_array(), tile_w)
+        assert (kept, tiles) == (want_kept, want_tiles), cfg.name
+
+
+def test_odd_row_stride_and_unaligned_planes(shading_ctx, gpu, env_map):
+    """Input rows wider than the frame (odd stride) and planes starting 4 bytes off an 8-byte
+    boundary: the pair kernel's scalar-load path. Compared with the oracle on the packed planes."""
+    cfg = S.CONFIGS[3].with_size(101, 37)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), env_map, n_threads=8)
+    shading_ctx.set_pass(pc)
+    shading_ctx.set_env_map(env_map)
+    big = np.full((15, 37, 103), np.nan, np.float32)  # row stride 103: odd
+    for c0 in (0, 1):  # c0 = 1: every plane starts 4 bytes off an 8-byte boundary
+        big[:] = np.nan
+        big[:, :, c0:c0 + 101] = planes
+        dev = torch.from_numpy(big).to(gpu)
+        view = GBuffer(dev[:, :, c0:], width=101)
+        assert view.row_stride == 103
+        got = shading_ctx.shade(view).cpu().numpy()
+        assert report(f"stride 103, column offset {c0}", got, ref).max() <= REL_TOL
+
+
 def test_culling_with_nonfinite_positions(shading_ctx, gpu):
     cfg = S.CONFIGS[4].with_size(256, 64)
     planes, _ = S.fill_gbuffer_host(cfg)
