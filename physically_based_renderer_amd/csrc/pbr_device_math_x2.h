@@ -7,12 +7,30 @@
 // seeds (v_rcp_f32, v_rsq_f32), compares, selects and the fp64 powf (pow5) have no packed form and run
 // per element. Pixels that leave the fast-path window are re-evaluated by the scalar exact path.
 #pragma once
+#include <cstdint>
+
 #include "pbr_device_math.h"
 
 namespace pbr {
 
 typedef float v2 __attribute__((ext_vector_type(2)));
-typedef int v2i __attribute__((ext_vector_type(2)));
+
+// Per-element conditions of the pair as wave lane masks (bit l = work-item l of the wave): a compare
+// writes its mask straight into an SGPR pair, and combining masks (the fast-path window, the redo
+// set) runs on the scalar unit instead of as v_cndmask / v_and / v_or on VGPR int vectors. Every
+// function below that builds or reads a mask is called by all lanes of the wave (uniform control flow).
+struct m2 {
+    uint64_t x, y;
+};
+__device__ __forceinline__ uint64_t lanes(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+__device__ __forceinline__ bool on(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+__device__ __forceinline__ m2 operator&(m2 a, m2 b) { return m2{a.x & b.x, a.y & b.y}; }
+__device__ __forceinline__ m2 operator|(m2 a, m2 b) { return m2{a.x | b.x, a.y | b.y}; }
+__device__ __forceinline__ m2 operator~(m2 a) { return m2{~a.x, ~a.y}; }
+__device__ __forceinline__ m2& operator&=(m2& a, m2 b) { return a = a & b; }
+__device__ __forceinline__ m2& operator|=(m2& a, m2 b) { return a = a | b; }
+__device__ __forceinline__ m2 mask2(bool x, bool y) { return m2{lanes(x), lanes(y)}; }
+__device__ __forceinline__ m2 all2(bool c) { const uint64_t m = lanes(c); return m2{m, m}; }
 
 struct f3x2 {
     v2 x, y, z;
@@ -22,7 +40,11 @@ __device__ __forceinline__ v2 vfma(v2 a, v2 b, v2 c) { return __builtin_elementw
 __device__ __forceinline__ v2 vmax(v2 a, v2 b) { return __builtin_elementwise_max(a, b); }  // IEEE maxNum
 __device__ __forceinline__ v2 vmin(v2 a, v2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ v2 vsat(v2 a) { return vmin(vmax(a, (v2)(0.0f)), (v2)(1.0f)); }
-__device__ __forceinline__ v2 vsel(v2i m, v2 a, v2 b) { return v2{m.x ? a.x : b.x, m.y ? a.y : b.y}; }
+__device__ __forceinline__ v2 vsel(m2 m, v2 a, v2 b) { return v2{on(m.x) ? a.x : b.x, on(m.y) ? a.y : b.y}; }
+__device__ __forceinline__ m2 ge(v2 a, float c) { return mask2(a.x >= c, a.y >= c); }
+__device__ __forceinline__ m2 le(v2 a, float c) { return mask2(a.x <= c, a.y <= c); }
+__device__ __forceinline__ m2 eq(v2 a, float c) { return mask2(a.x == c, a.y == c); }
+__device__ __forceinline__ m2 not_gt(v2 a, float c) { return mask2(!(a.x > c), !(a.y > c)); }
 __device__ __forceinline__ f3x2 add3(f3x2 a, f3x2 b) { return f3x2{a.x + b.x, a.y + b.y, a.z + b.z}; }
 // HLSL dot, same association as dot3: (a.x*b.x + a.y*b.y) + a.z*b.z
 __device__ __forceinline__ v2 dot3(f3x2 a, f3x2 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
@@ -50,16 +72,16 @@ __device__ __forceinline__ v2 sqrt_nr(v2 x) {  // see sqrt_nr in pbr_device_math
     return vfma(r, 0.5f * y, s0);
 }
 __device__ __forceinline__ v2 pow5_light(v2 x) { return v2{pow5_light(x.x), pow5_light(x.y)}; }
-// |x| in [lo, hi] per element (false for NaN), as an int mask (-1 / 0).
-__device__ __forceinline__ v2i in_win(v2 x, float lo, float hi) {
+// |x| in [lo, hi] per element (false for NaN).
+__device__ __forceinline__ m2 in_win(v2 x, float lo, float hi) {
     v2 a = __builtin_elementwise_abs(x);
-    return (a >= lo) & (a <= hi);
+    return ge(a, lo) & le(a, hi);
 }
 
 struct PixelInvariants2 {
     f3x2 n, v, albedo, f0, one_minus_f0;
     v2 one_minus_metal, a_sqr, a_sqr_minus_1, k, one_minus_k, ggx_v, four_n_dot_v;
-    v2i f0_nonzero;  // -1 where no F0 component is zero
+    m2 f0_nonzero;  // no F0 component is zero
 };
 
 // make_invariants (pbr_device_math.h) element-wise for the pair: the same operations, packed. The one
@@ -67,7 +89,7 @@ struct PixelInvariants2 {
 // pixels in the fast window (`fast`): roughness in [0, 1] puts k in [1/8, 1/2] and the denominator in
 // [2^-3, 2^5]; n_dot_v must be 0 or >= 2^-100 so the residual stays normal. Otherwise IEEE.
 __device__ __forceinline__ PixelInvariants2 make_invariants(const f3x2& n, const f3x2& v, const f3x2& albedo,
-                                                            const f3x2& f0, v2 metallic, v2 roughness, v2i fast) {
+                                                            const f3x2& f0, v2 metallic, v2 roughness, m2 fast) {
     PixelInvariants2 q;
     q.n = n;
     q.v = v;
@@ -84,15 +106,16 @@ __device__ __forceinline__ PixelInvariants2 make_invariants(const f3x2& n, const
     q.one_minus_k = 1.0f - q.k;
     v2 n_dot_v = vmax(dot3(n, v), splat(0.0f));
     const v2 den = n_dot_v * q.one_minus_k + q.k;
-    const v2i ok = fast & ((n_dot_v == 0.0f) | (n_dot_v >= 0x1p-100f));
+    const m2 ok = fast & (eq(n_dot_v, 0.0f) | ge(n_dot_v, 0x1p-100f));
     const v2 gq = div_nr(n_dot_v, recip_nr(den));
-    if (__builtin_expect(ok.x & ok.y, 1)) {
+    if (__builtin_expect(on(ok.x) && on(ok.y), 1)) {
         q.ggx_v = gq;
     } else {
-        q.ggx_v = v2{ok.x ? gq.x : n_dot_v.x / den.x, ok.y ? gq.y : n_dot_v.y / den.y};
+        q.ggx_v = v2{on(ok.x) ? gq.x : n_dot_v.x / den.x, on(ok.y) ? gq.y : n_dot_v.y / den.y};
     }
     q.four_n_dot_v = 4.0f * n_dot_v;
-    q.f0_nonzero = (f0.x != 0.0f) & (f0.y != 0.0f) & (f0.z != 0.0f);
+    q.f0_nonzero = mask2(f0.x.x != 0.0f && f0.y.x != 0.0f && f0.z.x != 0.0f,
+                         f0.x.y != 0.0f && f0.y.y != 0.0f && f0.z.y != 0.0f);
     return q;
 }
 
@@ -118,7 +141,7 @@ __device__ __forceinline__ PixelInvariants unpack_invariants(const PixelInvarian
     s.ggx_v = i ? q.ggx_v.y : q.ggx_v.x;
     s.four_n_dot_v = i ? q.four_n_dot_v.y : q.four_n_dot_v.x;
     s.fast_ok = false;
-    s.f0_nonzero = (i ? q.f0_nonzero.y : q.f0_nonzero.x) != 0;
+    s.f0_nonzero = on(i ? q.f0_nonzero.y : q.f0_nonzero.x);
     return s;
 }
 
@@ -126,12 +149,12 @@ __device__ __forceinline__ PixelInvariants unpack_invariants(const PixelInvarian
 // per-iteration window conditions (see pbr_device_math.h).
 __device__ __forceinline__ v2 div_pi(v2 x) { return vfma(x, splat(kInvPiHi), x * kInvPiLo); }  // see div_pi
 
-__device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, v2i& ok) {
+__device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, m2& ok) {
     v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
     v2 n_dot_h_sqr = n_dot_h * n_dot_h;
     v2 den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
     den = kPi * den * den;
-    ok &= (den >= 0x1p-60f) & (den <= 0x1p60f);
+    ok &= ge(den, 0x1p-60f) & le(den, 0x1p60f);
     v2 ndf = div_nr(q.a_sqr, recip_nr(den));
     v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
     v2 ggx_l = div_nr(n_dot_l, recip_nr(n_dot_l * q.one_minus_k + q.k));
@@ -142,7 +165,7 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance
     v2 ndf_g = ndf * g;
     v2 denom = q.four_n_dot_v * n_dot_l + 0.001f;
     f3x2 nom = f3x2{ndf_g * f.x, ndf_g * f.y, ndf_g * f.z};
-    ok &= ((ndf_g == 0.0f) | in_win(ndf_g, 0x1p-30f, 0x1p40f)) & (q.f0_nonzero | (p == 0.0f) | (p >= 0x1p-40f));
+    ok &= (eq(ndf_g, 0.0f) | in_win(ndf_g, 0x1p-30f, 0x1p40f)) & (q.f0_nonzero | eq(p, 0.0f) | ge(p, 0x1p-40f));
     const Recip2 rd = recip_nr(denom);
     f3x2 spec = f3x2{div_nr(nom.x, rd), div_nr(nom.y, rd), div_nr(nom.z, rd)};
     f3x2 kd = f3x2{(1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal};
@@ -151,15 +174,15 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance
                 ((div_pi(kd.z * q.albedo.z) + spec.z) * radiance.z) * n_dot_l};
 }
 
-__device__ __forceinline__ f3x2 normalize_x2(f3x2 v, v2i& ok) {
+__device__ __forceinline__ f3x2 normalize_x2(f3x2 v, m2& ok) {
     v2 s = sqrt_nr(dot3(v, v));
-    ok &= (s >= 0x1p-30f);  // s <= 1 + |L| <= 29 by the windows
+    ok &= ge(s, 0x1p-30f);  // s <= 1 + |L| <= 29 by the windows
     const Recip2 r = recip_nr(s);
     return f3x2{div_nr(v.x, r), div_nr(v.y, r), div_nr(v.z, r)};
 }
 
 // ComputeDirectionalLight, packed fast path.
-__device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, float4 s, float4 d, v2i& ok) {
+__device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, float4 s, float4 d, m2& ok) {
     f3x2 l = splat3(-d.x, -d.y, -d.z);
     f3x2 h = normalize_x2(add3(q.v, l), ok);
     return brdf_x2(q, splat3(s.x, s.y, s.z), l, h, ok);
@@ -169,11 +192,11 @@ __device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, float4
 // as in the scalar version). Lanes with lit == 0 carry garbage in `out` and are never added.
 template <bool SPOT>
 __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const f3x2& pos,
-                                                 float4 s, float4 d, float4 p, v2i& lit, v2i& ok) {
+                                                 float4 s, float4 d, float4 p, m2& lit, m2& ok) {
     f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
     v2 dist = sqrt_nr(dot3(l, l));
-    lit = !(dist > kLightRange);
-    ok &= (dist >= 0x1p-20f);
+    lit = not_gt(dist, kLightRange);
+    ok &= ge(dist, 0x1p-20f);
     const Recip2 rdist = recip_nr(dist);
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     f3x2 h = normalize_x2(add3(q.v, l), ok);

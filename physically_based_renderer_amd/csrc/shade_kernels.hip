@@ -123,9 +123,9 @@ __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, in
 // ComputeLighting (LightingUtil.hlsl:170-200) for both pixels of the pair on the packed fast path:
 // in-order sum from +0; `redo` collects pixels that left the fast-path window for a lit light.
 template <bool CULL>
-__device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, v2i fast_ok,
+__device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, m2 fast_ok,
                                               const float4* __restrict__ lights, const PassArgs& ps, Lds& s,
-                                              const TileBounds& tb, bool cull_enabled, v2i& redo, int& kept_total) {
+                                              const TileBounds& tb, bool cull_enabled, m2& redo, int& kept_total) {
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     for (int base = 0; base < ps.n_dir; base += kChunk) {  // directional: never culled
         const int cnt = min(kChunk, ps.n_dir - base);
@@ -134,7 +134,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         __syncthreads();
         for (int j = 0; j < cnt; ++j) {
             const float4* r = &s.light[3 * j];
-            v2i ok = fast_ok & (r[2].w != 0.0f ? -1 : 0);
+            m2 ok = fast_ok & all2(r[2].w != 0.0f);
             const f3x2 c = directional_x2(q, r[0], r[1], ok);
             redo |= ~ok;
             direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
@@ -155,8 +155,8 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
 #pragma unroll PBR_X2_LIGHT_UNROLL
             for (int j = 0; j < kept; ++j) {
                 const float4* r = &s.light[3 * j];
-                v2i ok = fast_ok & (r[2].w != 0.0f ? -1 : 0);
-                v2i lit;
+                m2 ok = fast_ok & all2(r[2].w != 0.0f);
+                m2 lit;
                 const f3x2 c = kind == 1 ? point_or_spot_x2<false>(q, pos, r[0], r[1], r[2], lit, ok)
                                          : point_or_spot_x2<true>(q, pos, r[0], r[1], r[2], lit, ok);
                 redo |= lit & ~ok;
@@ -360,16 +360,17 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                     p.metallic.x, p.roughness.x);
     const bool ok_b = !exact_only && ps.eye_ok && fast_window_ok(pb, lane(p.n, 1), lane(p.albedo, 1), lane(p.f0, 1),
                                                     p.metallic.y, p.roughness.y);
-    const v2i fast2 = v2i{ok_a ? -1 : 0, ok_b ? -1 : 0};
+    const m2 fast2 = mask2(ok_a, ok_b);
 
     // V = normalize(g_CameraPosW - pin.PosW)  (Default.hlsl:53). In the window every component of
     // eye - pos is 0 or >= 2^-44 and |eye - pos| < 2^22, so the exact fast normalize applies once
     // |V| >= 2^-30; other pixels take the IEEE sequences.
     const f3x2 ve = f3x2{ps.eye[0] - p.pos.x, ps.eye[1] - p.pos.y, ps.eye[2] - p.pos.z};
-    v2i okv = fast2;
+    m2 okv = fast2;
     f3x2 v = normalize_x2(ve, okv);
-    if (__builtin_expect(!(okv.x & okv.y), 0)) {
-        const f3 v0 = okv.x ? lane(v, 0) : normalize3(lane(ve, 0)), v1 = okv.y ? lane(v, 1) : normalize3(lane(ve, 1));
+    const bool va_ok = on(okv.x), vb_ok = on(okv.y);
+    if (__builtin_expect(!(va_ok && vb_ok), 0)) {
+        const f3 v0 = va_ok ? lane(v, 0) : normalize3(lane(ve, 0)), v1 = vb_ok ? lane(v, 1) : normalize3(lane(ve, 1));
         v = f3x2{v2{v0.x, v1.x}, v2{v0.y, v1.y}, v2{v0.z, v1.z}};
     }
     const PixelInvariants2 q2 = make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness, fast2);
@@ -409,17 +410,17 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     // lives only in packed form (q2, pos2); the scalar views are rebuilt from it afterwards so the
     // loop does not carry two copies of the invariants.
     int kept_total = 0;
-    v2i redo = v2i{0, 0};
+    m2 redo = m2{0, 0};
     const f3x2 pos2 = p.pos;
     const float ao_a = p.ao.x, ao_b = p.ao.y;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
     if (any_geometry) {  // block-uniform
-        d2 = lighting_fast<CULL>(q2, pos2, v2i{ok_a ? -1 : 0, ok_b ? -1 : 0}, lights, ps, s, tb, cull_enabled, redo,
+        d2 = lighting_fast<CULL>(q2, pos2, fast2, lights, ps, s, tb, cull_enabled, redo,
                                  kept_total);
     }
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
     f3 da = lane(d2, 0), db = lane(d2, 1);
-    const bool need_a = ga && redo.x != 0, need_b = gb_ && redo.y != 0;
+    const bool need_a = ga && on(redo.x), need_b = gb_ && on(redo.y);
     if (__syncthreads_or(need_a || need_b)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
         f3 ea, eb;
         lighting_exact<CULL>(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, s, tb, cull_enabled,
