@@ -149,12 +149,22 @@ __device__ __forceinline__ PixelInvariants unpack_invariants(const PixelInvarian
 // per-iteration window conditions (see pbr_device_math.h).
 __device__ __forceinline__ v2 div_pi(v2 x) { return vfma(x, splat(kInvPiHi), x * kInvPiLo); }  // see div_pi
 
+// LEAN: every pixel of the wave is inside the fast window with |N|^2 <= 1 + 2^-20 (dot3 as rounded)
+// and no zero F0 component; then two of the per-light window tests hold without being tested:
+//  * den: |N| <= 1 + 2^-20.9 and the fast normalize gives |H| <= 1 + 2^-21, so N.H <= 1 + 2^-19.6
+//    after the dot's roundings and n_dot_h^2 <= 1 + 2^-18.6; with roughness clamped to >= 0.05,
+//    a^2 >= 2^-17.29 and inner = n_dot_h^2 (a^2 - 1) + 1 >= a^2 - 2^-18.6 (1 - a^2) - 2^-23 >= 2^-18.1,
+//    inner <= 1, so den = pi inner^2 is in [2^-37, pi], inside [2^-60, 2^60];
+//  * with |F0| in [2^-20, 1024] (per-pixel window, no zero component), F = F0 + (1 - F0) p is either
+//    near F0 or an exact cancellation (a multiple of ulp(F0)/2 >= 2^-45), so F is 0 or >= 2^-45 and
+//    ndf_g F stays inside the division window for any p: the p == 0 / p >= 2^-40 test is moot.
+template <bool LEAN>
 __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, m2& ok) {
     v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
     v2 n_dot_h_sqr = n_dot_h * n_dot_h;
     v2 den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
     den = kPi * den * den;
-    ok &= ge(den, 0x1p-60f) & le(den, 0x1p60f);
+    if (!LEAN) ok &= ge(den, 0x1p-60f) & le(den, 0x1p60f);
     v2 ndf = div_nr(q.a_sqr, recip_nr(den));
     v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
     v2 ggx_l = div_nr(n_dot_l, recip_nr(n_dot_l * q.one_minus_k + q.k));
@@ -165,7 +175,8 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance
     v2 ndf_g = ndf * g;
     v2 denom = q.four_n_dot_v * n_dot_l + 0.001f;
     f3x2 nom = f3x2{ndf_g * f.x, ndf_g * f.y, ndf_g * f.z};
-    ok &= (eq(ndf_g, 0.0f) | in_win(ndf_g, 0x1p-30f, 0x1p40f)) & (q.f0_nonzero | eq(p, 0.0f) | ge(p, 0x1p-40f));
+    ok &= eq(ndf_g, 0.0f) | in_win(ndf_g, 0x1p-30f, 0x1p40f);
+    if (!LEAN) ok &= q.f0_nonzero | eq(p, 0.0f) | ge(p, 0x1p-40f);
     const Recip2 rd = recip_nr(denom);
     f3x2 spec = f3x2{div_nr(nom.x, rd), div_nr(nom.y, rd), div_nr(nom.z, rd)};
     f3x2 kd = f3x2{(1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal};
@@ -182,15 +193,16 @@ __device__ __forceinline__ f3x2 normalize_x2(f3x2 v, m2& ok) {
 }
 
 // ComputeDirectionalLight, packed fast path.
+template <bool LEAN>
 __device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, float4 s, float4 d, m2& ok) {
     f3x2 l = splat3(-d.x, -d.y, -d.z);
     f3x2 h = normalize_x2(add3(q.v, l), ok);
-    return brdf_x2(q, splat3(s.x, s.y, s.z), l, h, ok);
+    return brdf_x2<LEAN>(q, splat3(s.x, s.y, s.z), l, h, ok);
 }
 
 // ComputePointLight / ComputeSpotLight, packed fast path. `lit` = the range test passed (exact,
 // as in the scalar version). Lanes with lit == 0 carry garbage in `out` and are never added.
-template <bool SPOT>
+template <bool SPOT, bool LEAN>
 __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const f3x2& pos,
                                                  float4 s, float4 d, float4 p, m2& lit, m2& ok) {
     f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
@@ -206,7 +218,7 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
         v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
-    return brdf_x2(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
+    return brdf_x2<LEAN>(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
 }
 
 }  // namespace pbr

@@ -122,7 +122,8 @@ __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, in
 
 // ComputeLighting (LightingUtil.hlsl:170-200) for both pixels of the pair on the packed fast path:
 // in-order sum from +0; `redo` collects pixels that left the fast-path window for a lit light.
-template <bool CULL>
+// LEAN (wave-uniform): the wave's pixels satisfy the extra conditions of brdf_x2<true>.
+template <bool CULL, bool LEAN>
 __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, m2 fast_ok,
                                               const float4* __restrict__ lights, const PassArgs& ps, Lds& s,
                                               const TileBounds& tb, bool cull_enabled, m2& redo, int& kept_total) {
@@ -135,7 +136,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         for (int j = 0; j < cnt; ++j) {
             const float4* r = &s.light[3 * j];
             m2 ok = fast_ok & all2(r[2].w != 0.0f);
-            const f3x2 c = directional_x2(q, r[0], r[1], ok);
+            const f3x2 c = directional_x2<LEAN>(q, r[0], r[1], ok);
             redo |= ~ok;
             direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
         }
@@ -157,8 +158,8 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
                 const float4* r = &s.light[3 * j];
                 m2 ok = fast_ok & all2(r[2].w != 0.0f);
                 m2 lit;
-                const f3x2 c = kind == 1 ? point_or_spot_x2<false>(q, pos, r[0], r[1], r[2], lit, ok)
-                                         : point_or_spot_x2<true>(q, pos, r[0], r[1], r[2], lit, ok);
+                const f3x2 c = kind == 1 ? point_or_spot_x2<false, LEAN>(q, pos, r[0], r[1], r[2], lit, ok)
+                                         : point_or_spot_x2<true, LEAN>(q, pos, r[0], r[1], r[2], lit, ok);
                 redo |= lit & ~ok;
                 // An unlit light adds +0 in the reference (identity on a sum that is never -0).
                 direct = add3(direct, f3x2{vsel(lit, c.x, splat(0.0f)), vsel(lit, c.y, splat(0.0f)),
@@ -415,8 +416,14 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const float ao_a = p.ao.x, ao_b = p.ao.y;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
     if (any_geometry) {  // block-uniform
-        d2 = lighting_fast<CULL>(q2, pos2, fast2, lights, ps, s, tb, cull_enabled, redo,
-                                 kept_total);
+        // Wave-uniform choice of the light loop (both variants stage lights with the same barriers).
+        const v2 nn = dot3(p.n, p.n);
+        const bool lean_lane = ok_a && ok_b && nn.x <= 1.0f + 0x1p-20f && nn.y <= 1.0f + 0x1p-20f &&
+                               on(q2.f0_nonzero.x) && on(q2.f0_nonzero.y);
+        if (lanes(!lean_lane) == 0)
+            d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, s, tb, cull_enabled, redo, kept_total);
+        else
+            d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, s, tb, cull_enabled, redo, kept_total);
     }
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
     f3 da = lane(d2, 0), db = lane(d2, 1);
