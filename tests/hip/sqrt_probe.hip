@@ -55,6 +55,9 @@ __global__ void recip_sqrt_sweep(int which, int emin, int emax, unsigned long lo
         float r;
         if (which == 0) {  // Newton on 1/s from y
             r = __builtin_fmaf(__builtin_fmaf(-s, y, 1.0f), y, y);
+        } else if (which == 2) {  // two Newton steps on 1/s from y (no v_rcp)
+            const float r1 = __builtin_fmaf(__builtin_fmaf(-s, y, 1.0f), y, y);
+            r = __builtin_fmaf(__builtin_fmaf(-s, r1, 1.0f), r1, r1);
         } else {           // control: v_rcp(s) + Newton (the current path)
             const float r0 = __builtin_amdgcn_rcpf(s);
             r = __builtin_fmaf(__builtin_fmaf(-s, r0, 1.0f), r0, r0);

@@ -14,7 +14,7 @@ for w in range(4):
     rc = L.probe_sqrt(w, -64, 64, ctypes.byref(bad), ctypes.byref(first))
     print(f"{names[w]:18s} exponents [-64,64]: rc {rc} mismatches {bad.value} of {129 << 23} first {first.value:#x}",
           flush=True)
-for w, name in enumerate(["1/s by Newton from rsq seed", "1/s by v_rcp + Newton"]):
+for w, name in enumerate(["1/s by Newton from rsq seed", "1/s by v_rcp + Newton", "1/s by 2 Newton from rsq"]):
     bad, first = ctypes.c_ulonglong(), ctypes.c_uint()
     rc = L.probe_recip_sqrt(w, -64, 64, ctypes.byref(bad), ctypes.byref(first))
     print(f"{name:30s} t exponents [-64,64]: rc {rc} mismatches {bad.value} first {first.value:#x}", flush=True)
