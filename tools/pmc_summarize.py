@@ -65,6 +65,24 @@ def main():
         "source": f"profiles/{tag}/pmc_*_{workload}.csv (rocprofv3 --pmc, separate passes, bench.py --steps 5)",
         "kernel_revision": revision,
     }
+    # Kernel trace of the bench run itself: mean launch time over the timed steps (the last K launches;
+    # the clock-ramp and warm-up launches come first) next to the bench's own HIP-event average.
+    trace = find(f"{src}/kt/**/*kernel_trace.csv")
+    shutil.copy(trace, os.path.join(dst, f"kernel_trace_{workload}.csv"))
+    with open(trace) as f:
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in csv.DictReader(f)
+                if "shade_tile" in r["Kernel_Name"]]
+    bench = None
+    for line in open(os.path.join(src, "kt.log")):
+        if line.startswith("{"):
+            bench = json.loads(line)
+    k = bench["steps"] if bench else len(durs)
+    entry["kernel_trace"] = {
+        "launches": len(durs), "mean_ms_all": sum(durs) / len(durs),
+        "mean_ms_timed_steps": sum(durs[-k:]) / k, "timed_steps": k,
+        "bench_avg_launch_ms": bench["roofline"]["avg_launch_ms"] if bench else None,
+        "bench_value": bench["value"] if bench else None,
+    }
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     summary = json.load(open(path)) if os.path.exists(path) else {}
     summary[workload] = entry

@@ -21,7 +21,7 @@ run() {  # name, timeout, command...
   return $rc
 }
 run kt 300 rocprofv3 --kernel-trace --stats -d "$out/kt" -o kt --output-format csv -- python3 bench.py "$@" &&
-run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_fetch" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@" &&
-run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$out/pmc_write" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@" &&
-run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$out/pmc_sq" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@" &&
-run pmc_busy 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES -d "$out/pmc_busy" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@"
+run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_fetch" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 1 --ramp-ms 0 --no-cpu-baseline "$@" &&
+run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$out/pmc_write" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 1 --ramp-ms 0 --no-cpu-baseline "$@" &&
+run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$out/pmc_sq" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 1 --ramp-ms 0 --no-cpu-baseline "$@" &&
+run pmc_busy 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES -d "$out/pmc_busy" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 1 --ramp-ms 0 --no-cpu-baseline "$@"
