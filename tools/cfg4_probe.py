@@ -19,21 +19,21 @@ sys.path.insert(0, ROOT)
 from physically_based_renderer_amd import _native as N  # noqa: E402
 from physically_based_renderer_amd import scenes as S  # noqa: E402
 from physically_based_renderer_amd.renderer import GBuffer, PassConstants, ShadingContext  # noqa: E402
+from clock_ramp import clock_ramp  # noqa: E402
 
 
 def time_pass(ctx, gb, out, pc, reps):
+    """Median launch time of `reps` back-to-back passes (events recorded between launches, one sync)."""
     ctx.set_pass(pc)
     for _ in range(3):
         ctx.shade(gb, out)
-    ts = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record()
         ctx.shade(gb, out)
-        b.record()
-        b.synchronize()
-        ts.append(a.elapsed_time(b))
-    return float(np.median(ts))
+        e1.record()
+    torch.cuda.synchronize()
+    return float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
 
 
 def tile_survivors(planes, lights, tw=64, th=8, radius=100.01):
@@ -78,6 +78,8 @@ def main():
         ("0 lights, metallic workflow", pc(lights, 0, 0)),
     ]
     with ShadingContext(0) as ctx:
+        ctx.set_pass(rows[0][1])
+        clock_ramp(ctx, gb, out)
         for name, p in rows:
             ms = time_pass(ctx, gb, out, p, a.reps)
             extra = ""

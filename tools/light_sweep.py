@@ -15,6 +15,7 @@ sys.path.insert(0, ROOT)
 from physically_based_renderer_amd import _native as N  # noqa: E402
 from physically_based_renderer_amd import scenes as S  # noqa: E402
 from physically_based_renderer_amd.renderer import GBuffer, PassConstants, ShadingContext  # noqa: E402
+from clock_ramp import clock_ramp  # noqa: E402
 
 
 def main():
@@ -34,6 +35,8 @@ def main():
     px = a.width * a.height
     with ShadingContext(0) as ctx:
         ctx.set_env_map(S.env_map())
+        ctx.set_pass(base)
+        clock_ramp(ctx, gb, out)
         prev = None
         for n in (0, 1, 2, 4, 8, 16, 32, 64):
             pc = PassConstants(eye_pos_w=base.eye_pos_w, num_point_lights=n, lights_array=lights[:max(n, 1)],
