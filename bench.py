@@ -58,10 +58,10 @@ def bytes_per_pixel(pc, out_bytes: int = 16) -> int:
     return planes * 4 + out_bytes
 
 
-def flops_per_pixel(pc, lights_per_tile=None, tile_px: int = 512) -> float:
+def flops_per_pixel(pc, lights_per_tile=None, tile_px: int = 128) -> float:
     """Algorithmic FLOP per pixel. With tiled culling only the lights that survive a tile are shaded
     (base + L_in per-light BRDFs); the 9-FLOP range test of every point/spot light is
-    counted once per tile (the unit that runs it), not per pixel, so skipped work is never counted."""
+    counted once per culling tile (the unit that runs it), not per pixel, so skipped work is never counted."""
     n_ps = pc.num_point_lights + pc.num_spot_lights
     f = FLOP_BASE + FLOP_HOIST
     if pc.flags & N.PBR_FLAG_TILED_CULLING and lights_per_tile is not None:
@@ -288,7 +288,7 @@ def main():
         bpp = bytes_per_pixel(pc, 4 if rgba8 else 16)
         achieved = bpp * band_px / avg_kernel_s / 1e9
         traffic, valu_busy = load_pmc(workload)
-        tile_px = 256 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 512  # 32x8 or 64x8 tiles
+        tile_px = 256 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 128  # culling unit: 32x8 / 64x2
         fpp = flops_per_pixel(pc, cull_note.get("lights_per_tile"), tile_px)
         tflops = fpp * band_px / avg_kernel_s / 1e12
         # At 64 lights the arithmetic intensity (fpp / bpp ~ 99 FLOP/B) is 5x the ridge point, so the

@@ -160,8 +160,10 @@ int pbr_set_sky_map_f32(pbr_context* ctx, const float* texels, int32_t width, in
 int pbr_shade_frame(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* frame, void* stream);
 
 /* Tiled-culling statistics of the last culled pass on `stream` (synchronises that stream):
- * total surviving point/spot lights summed over the tiles that hold geometry, and the number of those
- * tiles. The kernel writes one count per tile (no atomics); this call sums them on the host. */
+ * total surviving point/spot lights summed over the culling tiles that hold geometry, and the number
+ * of those tiles. A culling tile is one wave64's pixels (64x2 in the default pixel-pair layout, 32x8
+ * workgroups in the one-pixel layout). The kernel writes per-workgroup counts (no atomics); this
+ * call sums them on the host. */
 int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream);
 
 /* ---- Host G-buffer fill (replaces the VS + rasteriser front-end, Default.hlsl:22-45) ---------- */

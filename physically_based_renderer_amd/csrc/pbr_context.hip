@@ -181,6 +181,21 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
             if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass ring wait");
         }
         std::memcpy(ctx->h_ring[slot], pass->lights, sizeof(pbr_light) * (size_t)n);
+        // The kernel's per-light fast-path flag travels in the unused pad1 of the uploaded copy
+        // (the caller's array is not touched): directional L = -Direction components, point / spot
+        // positions, each 0 or |x| in [2^-20, 16] / [2^-20, 2^20] (pbr_device_math.h, light_window_ok).
+        for (long long i = 0; i < n; ++i) {
+            pbr_light& L = ctx->h_ring[slot][i];
+            const bool directional = i < nd;
+            const float* c = directional ? L.direction : L.position;
+            const float hi = directional ? 16.0f : 0x1p20f;
+            bool ok = true;
+            for (int k = 0; k < 3; ++k) {
+                const float a = std::fabs(c[k]);
+                ok = ok && (a == 0.0f || (a >= 0x1p-20f && a <= hi));
+            }
+            L.pad1 = ok ? 1.0f : 0.0f;
+        }
         e = hipMemcpyAsync(ctx->d_lights, ctx->h_ring[slot], sizeof(pbr_light) * (size_t)n, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass copy");
         e = hipEventRecord(ctx->ring_done[slot], s);
@@ -324,7 +339,7 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
                 ctx->d_tile_kept = nullptr;
                 ctx->tile_kept_capacity = 0;
             }
-            e = hipMalloc(&ctx->d_tile_kept, sizeof(int32_t) * (size_t)tiles);
+            e = hipMalloc(&ctx->d_tile_kept, 2 * sizeof(int32_t) * (size_t)tiles);
             if (e != hipSuccess) return fail_hip(ctx, e, "cull stats hipMalloc");
             ctx->tile_kept_capacity = tiles;
         }
@@ -381,15 +396,14 @@ int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num
     *num_tiles = 0;
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (ctx->last_cull_tiles == 0) return PBR_OK;  // no culled pass yet
-    std::vector<int32_t> h((size_t)ctx->last_cull_tiles);
+    std::vector<int32_t> h(2 * (size_t)ctx->last_cull_tiles);
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e = hipMemcpyAsync(h.data(), ctx->d_tile_kept, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail_hip(ctx, e, "pbr_last_cull_stats");
-    for (int32_t k : h) {
-        if (k < 0) continue;  // tile without geometry (sky only): not shaded, not counted
-        *sum_tile_lights += k;
-        *num_tiles += 1;
+    for (size_t t = 0; t < h.size(); t += 2) {  // [survivors, culling units with geometry] per workgroup
+        *sum_tile_lights += h[t];
+        *num_tiles += h[t + 1];
     }
     return PBR_OK;
 }

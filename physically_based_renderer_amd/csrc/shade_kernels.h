@@ -49,9 +49,10 @@ struct LaunchArgs {
     const float4* lights;  // 3 float4 per light (the reference's 48-byte Light)
     const float4* env;     // env_w * env_h RGBA fp32, or nullptr
     FrameArgs frame;
-    // CULL only: one slot per tile (blockIdx.y * gridDim.x + blockIdx.x) receives the tile's surviving
-    // point/spot light count, or -1 for a tile with no geometry (plain stores: one same-address atomic
-    // per tile serialised the whole grid, 0.29 ms per 4K frame).
+    // CULL only: two ints per workgroup (blockIdx.y * gridDim.x + blockIdx.x): surviving point/spot
+    // lights summed over its culling units, and the number of culling units with geometry (the pair
+    // layout culls per wave = 64x2 pixels, the one-pixel layout per workgroup = 32x8). Plain stores:
+    // one same-address global atomic per tile serialised the whole grid (0.29 ms per 4K frame).
     int32_t* tile_kept;
     int ambient_mode;
     bool f0_plane, apply_ao, cull;

@@ -65,6 +65,7 @@ struct Lds {
     float4 light[3 * kChunk];
     int wave_cnt[kBlock / 64];
     float bounds[kBlock / 64][6];
+    int kept_sum, geo_waves;  // tiled-culling statistics of the block
 };
 
 // Stage lights [begin, begin+count) of the global list into LDS, culled against the tile when CULL.
@@ -120,50 +121,74 @@ __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, in
     return total;
 }
 
+// Light j's record as uploaded (the reference's 48-byte Light; pbr_set_pass stores the light's
+// fast-path window flag in the unused pad1 = .w of the position). The index is wave-uniform, so
+// these are scalar loads through the scalar cache: no LDS staging, no barrier.
+struct LightRec {
+    float4 s, d, p;
+};
+__device__ __forceinline__ LightRec light_rec(const float4* __restrict__ lights, int j) {
+    return LightRec{lights[3 * j], lights[3 * j + 1], lights[3 * j + 2]};
+}
+__device__ __forceinline__ float uniform_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+}
+
 // ComputeLighting (LightingUtil.hlsl:170-200) for both pixels of the pair on the packed fast path:
 // in-order sum from +0; `redo` collects pixels that left the fast-path window for a lit light.
 // LEAN (wave-uniform): the wave's pixels satisfy the extra conditions of brdf_x2<true>.
+// CULL: wave-level tiled culling. Each round, lane l range-tests point/spot light base + l against
+// the wave's own world-space box `wb` (its 64x2 pixels); the ballot of the survivors is walked in
+// increasing bit order, so the kept lights are summed in the reference's order. A dropped light is
+// one the reference's `d > 100` test (LightingUtil.hlsl:131) rejects for every pixel of the wave, i.e.
+// a +0 term: the result is bit-identical to the unculled pass.
 template <bool CULL, bool LEAN>
 __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, m2 fast_ok,
-                                              const float4* __restrict__ lights, const PassArgs& ps, Lds& s,
-                                              const TileBounds& tb, bool cull_enabled, m2& redo, int& kept_total) {
+                                              const float4* __restrict__ lights, const PassArgs& ps,
+                                              const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total) {
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
-    for (int base = 0; base < ps.n_dir; base += kChunk) {  // directional: never culled
-        const int cnt = min(kChunk, ps.n_dir - base);
-        __syncthreads();
-        stage_chunk<false>(lights, base, cnt, s, tb, false, true);
-        __syncthreads();
-        for (int j = 0; j < cnt; ++j) {
-            const float4* r = &s.light[3 * j];
-            m2 ok = fast_ok & all2(r[2].w != 0.0f);
-            const f3x2 c = directional_x2<LEAN>(q, r[0], r[1], ok);
-            redo |= ~ok;
-            direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
-        }
+    for (int j = 0; j < ps.n_dir; ++j) {  // directional: never culled
+        const LightRec r = light_rec(lights, j);
+        m2 ok = fast_ok & all2(r.p.w != 0.0f);
+        const f3x2 c = directional_x2<LEAN>(q, r.s, r.d, ok);
+        redo |= ~ok;
+        direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
     }
     const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
+    auto point = [&](int kind, int j) {
+        const LightRec r = light_rec(lights, j);
+        m2 ok = fast_ok & all2(r.p.w != 0.0f);
+        m2 lit;
+        const f3x2 c = kind == 1 ? point_or_spot_x2<false, LEAN>(q, pos, r.s, r.d, r.p, lit, ok)
+                                 : point_or_spot_x2<true, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
+        redo |= lit & ~ok;
+        // An unlit light adds +0 in the reference (identity on a sum that is never -0).
+        direct = add3(direct, f3x2{vsel(lit, c.x, splat(0.0f)), vsel(lit, c.y, splat(0.0f)),
+                                   vsel(lit, c.z, splat(0.0f))});
+    };
 #pragma unroll 1
     for (int kind = 1; kind <= 2; ++kind) {
         const int b0 = kind == 1 ? pt_begin : sp_begin, b1 = kind == 1 ? sp_begin : end;
-        for (int base = b0; base < b1; base += kChunk) {
-            const int cnt = min(kChunk, b1 - base);
-            __syncthreads();
-            const int kept = stage_chunk<CULL>(lights, base, cnt, s, tb, cull_enabled, false);
-            __syncthreads();
-            kept_total += kept;
-            // PBR_X2_LIGHT_UNROLL > 1 lets the scheduler interleave lights (measured: no gain, the
-            // loop is VALU-throughput bound, not wait-state bound).
-#pragma unroll PBR_X2_LIGHT_UNROLL
-            for (int j = 0; j < kept; ++j) {
-                const float4* r = &s.light[3 * j];
-                m2 ok = fast_ok & all2(r[2].w != 0.0f);
-                m2 lit;
-                const f3x2 c = kind == 1 ? point_or_spot_x2<false, LEAN>(q, pos, r[0], r[1], r[2], lit, ok)
-                                         : point_or_spot_x2<true, LEAN>(q, pos, r[0], r[1], r[2], lit, ok);
-                redo |= lit & ~ok;
-                // An unlit light adds +0 in the reference (identity on a sum that is never -0).
-                direct = add3(direct, f3x2{vsel(lit, c.x, splat(0.0f)), vsel(lit, c.y, splat(0.0f)),
-                                           vsel(lit, c.z, splat(0.0f))});
+        if (!CULL) {
+            for (int j = b0; j < b1; ++j) point(kind, j);
+            continue;
+        }
+        for (int base = b0; base < b1; base += 64) {
+            const int j = base + (int)(threadIdx.x & 63);
+            bool keep = j < b1;
+            if (keep && cull_enabled) {
+                const float4 lp = lights[3 * j + 2];
+                const float dx = hmax(hmax(wb.mn[0] - lp.x, lp.x - wb.mx[0]), 0.0f);
+                const float dy = hmax(hmax(wb.mn[1] - lp.y, lp.y - wb.mx[1]), 0.0f);
+                const float dz = hmax(hmax(wb.mn[2] - lp.z, lp.z - wb.mx[2]), 0.0f);
+                keep = (dx * dx + dy * dy + dz * dz) <= kCullRadius * kCullRadius;
+            }
+            uint64_t m = lanes(keep);
+            kept_total += __popcll(m);
+            while (m) {
+                const int jl = base + __builtin_ctzll(m);
+                m &= m - 1;
+                point(kind, jl);
             }
         }
     }
@@ -340,6 +365,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                             bool exact_only) {
     __shared__ Lds s;
     load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
+    if (threadIdx.x == 0) s.kept_sum = s.geo_waves = 0;
     __syncthreads();
 
     const int tid = threadIdx.x;
@@ -351,7 +377,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     // Geometry (PS) or background (sky pass) per pixel; background pixels take no part in the tile
     // bounds, the exact re-pass or the lighting (a block without geometry skips it).
     const bool ga = va && is_geometry(fr, xa, y), gb_ = vb && is_geometry(fr, xa + 1, y);
-    const bool any_geometry = fr.coverage == nullptr || __syncthreads_or(ga || gb_);
+    const bool wave_geometry = lanes(ga || gb_) != 0;  // waves wholly outside the frame skip lighting
 
     const PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
                                                    vb && gb.pairs_aligned);
@@ -376,35 +402,22 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     }
     const PixelInvariants2 q2 = make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness, fast2);
 
-    TileBounds tb{};
+    // The wave's world-space box (its 64x2 pixels; background pixels excluded): wave64 butterflies,
+    // then scalar registers. Non-finite positions disable culling for the wave (the reference's
+    // NaN/inf behaviour at LightingUtil.hlsl:131 is then reproduced light by light).
+    TileBounds wb{};
     bool cull_enabled = false;
     if (CULL) {
         const bool finite = (!ga || (isfinite(pa.x) && isfinite(pa.y) && isfinite(pa.z))) &&
                             (!gb_ || (isfinite(pb.x) && isfinite(pb.y) && isfinite(pb.z)));
         const float big = 3.0e38f;
-        float b[6];
-        b[0] = fminf(ga ? pa.x : big, gb_ ? pb.x : big);
-        b[1] = fminf(ga ? pa.y : big, gb_ ? pb.y : big);
-        b[2] = fminf(ga ? pa.z : big, gb_ ? pb.z : big);
-        b[3] = fmaxf(ga ? pa.x : -big, gb_ ? pb.x : -big);
-        b[4] = fmaxf(ga ? pa.y : -big, gb_ ? pb.y : -big);
-        b[5] = fmaxf(ga ? pa.z : -big, gb_ ? pb.z : -big);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) b[i] = wave_min(b[i]);
-#pragma unroll
-        for (int i = 3; i < 6; ++i) b[i] = wave_max(b[i]);
-        if ((tid & 63) == 0) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) s.bounds[tid >> 6][i] = b[i];
-        }
-        // Non-finite positions in the tile disable culling (the reference's NaN/inf behaviour at
-        // LightingUtil.hlsl:131 is then reproduced light by light).
-        cull_enabled = __syncthreads_and(finite) != 0;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            tb.mn[i] = fminf(fminf(s.bounds[0][i], s.bounds[1][i]), fminf(s.bounds[2][i], s.bounds[3][i]));
-            tb.mx[i] = fmaxf(fmaxf(s.bounds[0][i + 3], s.bounds[1][i + 3]), fmaxf(s.bounds[2][i + 3], s.bounds[3][i + 3]));
-        }
+        wb.mn[0] = uniform_f(wave_min(fminf(ga ? pa.x : big, gb_ ? pb.x : big)));
+        wb.mn[1] = uniform_f(wave_min(fminf(ga ? pa.y : big, gb_ ? pb.y : big)));
+        wb.mn[2] = uniform_f(wave_min(fminf(ga ? pa.z : big, gb_ ? pb.z : big)));
+        wb.mx[0] = uniform_f(wave_max(fmaxf(ga ? pa.x : -big, gb_ ? pb.x : -big)));
+        wb.mx[1] = uniform_f(wave_max(fmaxf(ga ? pa.y : -big, gb_ ? pb.y : -big)));
+        wb.mx[2] = uniform_f(wave_max(fmaxf(ga ? pa.z : -big, gb_ ? pb.z : -big)));
+        cull_enabled = lanes(!finite) == 0;
     }
 
     // ComputeLighting (LightingUtil.hlsl:170-200) on the packed fast path. From here on the pair
@@ -415,28 +428,35 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const f3x2 pos2 = p.pos;
     const float ao_a = p.ao.x, ao_b = p.ao.y;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
-    if (any_geometry) {  // block-uniform
-        // Wave-uniform choice of the light loop (both variants stage lights with the same barriers).
+    if (wave_geometry) {  // wave-uniform
+        // Wave-uniform choice of the light loop.
         const v2 nn = dot3(p.n, p.n);
         const bool lean_lane = ok_a && ok_b && nn.x <= 1.0f + 0x1p-20f && nn.y <= 1.0f + 0x1p-20f &&
                                on(q2.f0_nonzero.x) && on(q2.f0_nonzero.y);
         if (lanes(!lean_lane) == 0)
-            d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, s, tb, cull_enabled, redo, kept_total);
+            d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
         else
-            d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, s, tb, cull_enabled, redo, kept_total);
+            d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+        if (CULL && (tid & 63) == 0) {  // per-tile statistics: survivors summed over the block's waves
+            atomicAdd(&s.kept_sum, kept_total);
+            atomicAdd(&s.geo_waves, 1);
+        }
     }
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
     f3 da = lane(d2, 0), db = lane(d2, 1);
     const bool need_a = ga && on(redo.x), need_b = gb_ && on(redo.y);
     if (__syncthreads_or(need_a || need_b)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
         f3 ea, eb;
-        lighting_exact<CULL>(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, s, tb, cull_enabled,
-                             ea, eb);
+        lighting_exact<false>(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, s, TileBounds{},
+                              false, ea, eb);
         if (need_a) da = ea;
         if (need_b) db = eb;
     }
-    if (CULL && tid == 0 && tile_kept != nullptr)
-        tile_kept[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = any_geometry ? kept_total : -1;
+    if (CULL && tid == 0 && tile_kept != nullptr) {  // after the barrier above: every wave has added
+        const int64_t t = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        tile_kept[2 * t] = s.kept_sum;
+        tile_kept[2 * t + 1] = s.geo_waves;
+    }
 
     const int64_t orow = (int64_t)y * fr.out_stride;
     if (va)
@@ -570,8 +590,11 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
         lighting_exact<CULL>(q, q, pos, pos, need, false, lights, ps, s, tb, cull_enabled, e, unused);
         if (need) direct = e;
     }
-    if (CULL && tid == 0 && tile_kept != nullptr)
-        tile_kept[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = any_geometry ? kept_total : -1;
+    if (CULL && tid == 0 && tile_kept != nullptr) {  // this layout culls per block (32x8 pixels)
+        const int64_t t = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        tile_kept[2 * t] = any_geometry ? kept_total : 0;
+        tile_kept[2 * t + 1] = any_geometry ? 1 : 0;
+    }
     if (valid)
         store_pixel(fr, (int64_t)y * fr.out_stride + x,
                     geom ? finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env, q.fast_ok)

@@ -118,7 +118,7 @@ def test_all_background_and_culled_mixed(shading_ctx, gpu):
     assert O.bit_equal(got, ref).all()
     rng = np.random.default_rng(3)
     cov = np.ones((64, 512), np.uint8)
-    cov[:, 128:256] = 0  # two whole 64x8 tile columns of sky
+    cov[:, 128:256] = 0  # two whole 64-pixel tile columns of sky
     cov[rng.uniform(size=cov.shape) < 0.1] = 0
     planes[0:3, cov == 0] = np.nan  # background positions are never read for shading or culling
     culled = run_frame(shading_ctx, gpu, planes, pc, None, sky, cov, N.PBR_OUTPUT_RGBA32F)
@@ -126,8 +126,8 @@ def test_all_background_and_culled_mixed(shading_ctx, gpu):
     pc_full = PassConstants(**{**pc.__dict__, "flags": pc.flags & ~N.PBR_FLAG_TILED_CULLING})
     full = run_frame(shading_ctx, gpu, planes, pc_full, None, sky, cov, N.PBR_OUTPUT_RGBA32F)
     assert O.bit_equal(culled, full).all()
-    tile_w = 32 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 64
-    assert tiles == (512 // tile_w) * 8 - (128 // tile_w) * 8  # the all-sky tiles did no lighting
+    tile_w, tile_h = (32, 8) if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else (64, 2)  # culling unit
+    assert tiles == (512 // tile_w - 128 // tile_w) * (64 // tile_h)  # the all-sky tiles did no lighting
     ref = O.shade_frame(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, sky, cov,
                         O.OUTPUT_RGBA32F, n_threads=8)
     check(culled, ref, cov, N.PBR_OUTPUT_RGBA32F, "cfg4 strip, sky tiles + NaN background, culled")

@@ -93,14 +93,19 @@ def test_tiled_culling_is_bit_exact(shading_ctx, gpu):
     full = shading_ctx.shade(gb)
     torch.cuda.synchronize()
     assert O.bit_equal(culled.cpu().numpy(), full.cpu().numpy()).all()
-    tile_w = 32 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 64
-    assert tiles == ((cfg.width + tile_w - 1) // tile_w) * ((cfg.height + 7) // 8)
+    tile_w, tile_h = cull_tile()
+    assert tiles == ((cfg.width + tile_w - 1) // tile_w) * ((cfg.height + tile_h - 1) // tile_h)
     mean_kept = kept / tiles
-    print(f"cfg4 tiled culling: {mean_kept:.2f} of {cfg.n_lights} lights per {tile_w}x8 tile")
+    print(f"cfg4 tiled culling: {mean_kept:.2f} of {cfg.n_lights} lights per {tile_w}x{tile_h} tile")
     assert 0 < mean_kept < cfg.n_lights / 4
 
 
-def host_tile_survivors(planes, lights, tile_w, tile_h=8):
+def cull_tile():
+    """The culling unit: one wave64's pixels (64x2 pairs) or one 32x8 workgroup (one-pixel layout)."""
+    return (32, 8) if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else (64, 2)
+
+
+def host_tile_survivors(planes, lights, tile_w, tile_h):
     """The kernel's per-tile range test (shade_kernels.hip, stage_chunk) emulated in float32: box
     distance per axis with maxNum, (dx*dx + dy*dy) + dz*dz rounded per operation, <= 100.01f^2."""
     h, w = planes.shape[1:]
@@ -121,14 +126,14 @@ def host_tile_survivors(planes, lights, tile_w, tile_h=8):
 def test_cull_stats_equal_host_emulation(shading_ctx, gpu):
     """pbr_last_cull_stats (one count per tile, summed on the host) equals the range test emulated on
     the host, at the full config-4 size and on a ragged frame."""
-    tile_w = 32 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 64
+    tile_w, tile_h = cull_tile()
     for cfg in (S.CONFIGS[4], S.CONFIGS[4].with_size(1000, 203)):
         planes, _ = S.fill_gbuffer_host(cfg)
         pc = S.scene_pass(cfg)
         shading_ctx.set_pass(pc)
         shading_ctx.shade(GBuffer.from_host(planes, gpu))
         kept, tiles = shading_ctx.cull_stats()
-        want_kept, want_tiles = host_tile_survivors(planes, pc.light_array(), tile_w)
+        want_kept, want_tiles = host_tile_survivors(planes, pc.light_array(), tile_w, tile_h)
         assert (kept, tiles) == (want_kept, want_tiles), cfg.name
 
 

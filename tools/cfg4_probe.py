@@ -36,7 +36,7 @@ def time_pass(ctx, gb, out, pc, reps):
     return float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
 
 
-def tile_survivors(planes, lights, tw=64, th=8, radius=100.01):
+def tile_survivors(planes, lights, tw=64, th=2, radius=100.01):
     h, w = planes.shape[1:]
     p = planes[0:3].reshape(3, h // th, th, w // tw, tw)
     lo = p.min(axis=(2, 4)).reshape(3, -1).T
@@ -74,6 +74,7 @@ def main():
     rows = [
         ("cfg4 as benchmarked", pc(lights, 256, f0c)),
         ("all 256 lights culled away", pc(far, 256, f0c)),
+        ("0 lights, F0 plane, culling on", pc(lights, 0, f0c)),
         ("0 lights, F0 plane", pc(lights, 0, N.PBR_FLAG_F0_PLANE)),
         ("0 lights, metallic workflow", pc(lights, 0, 0)),
     ]
