@@ -133,6 +133,9 @@ def main():
                          "profiles/r01 kernel trace); not a step, no gather")
     ap.add_argument("--config", type=int, default=0, help="BASELINE config id (default 3 at N=1, 5 at N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rows-per-rank", type=int, default=1024,
+                    help="config 5 band height per rank at N > 1 (1024 = the BASELINE geometry; smaller only "
+                         "for rehearsing the multi-rank path)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the benchmark); gloo = host-staged gather, for exercising the "
                          "multi-rank path on one GPU")
@@ -158,7 +161,7 @@ def main():
     cid = args.config or (3 if world == 1 else 5)
     cfg = S.CONFIGS[cid]
     if world > 1 and cid == 5:
-        cfg = cfg.with_size(8192, 1024 * world)  # 1024 rows per rank; 8192x8192 at N = 8
+        cfg = cfg.with_size(8192, args.rows_per_rank * world)  # 1024 rows per rank: 8192x8192 at N = 8
     band = D.band_rows(cfg.height, world, rank)
     workload = f"{cfg.name}" + (f"_rows{cfg.height}" if cfg.height != S.CONFIGS[cid].height else "")
 

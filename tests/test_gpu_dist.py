@@ -1,0 +1,104 @@
+"""The multi-rank path with the HIP kernel: several ranks share the one GPU of the test box (gloo,
+host-staged gather; the benchmark itself uses RCCL, one GPU per rank).
+
+SURVEY §4 item 6: the gathered image must equal the single-GPU image bit for bit, run as 8 ranks over
+fewer devices. Also rehearses bench.py's own N > 1 leg (partition, pipelined gather, band checksums,
+max-over-ranks timing) under torch.distributed.run.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+WIDTH, HEIGHT = 200, 203  # ragged: bands of 8-row tiles plus a short tail
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from physically_based_renderer_amd import dist as D
+    from physically_based_renderer_amd import scenes as S
+    from physically_based_renderer_amd.renderer import ShadingContext
+
+    D.init_from_env("gloo")
+    dev = torch.device("cuda", 0)
+    cfg = S.CONFIGS[3].with_size(WIDTH, HEIGHT)
+    band = D.band_rows(cfg.height, world, rank)
+    gb = S.build_gbuffer(cfg, dev, band.row_begin, band.row_end, n_threads=2)
+    slot = torch.zeros((band.rows_max, cfg.width, 4), dtype=torch.float32, device=dev)
+    with ShadingContext(0) as ctx:
+        ctx.set_pass(S.scene_pass(cfg))
+        ctx.set_env_map(S.env_map())
+        ctx.shade(gb, slot[: band.rows])
+        torch.cuda.synchronize()
+    g = D.BandGather(band, cfg.width, dev)
+    D.BandGather.wait(g.start(slot))
+    frame = g.assembled(cfg.height)
+    if rank == 0:
+        q.put(frame.cpu().numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_eight_ranks_on_one_gpu_equal_single_frame(gpu):
+    from physically_based_renderer_amd import scenes as S
+    from physically_based_renderer_amd.renderer import ShadingContext
+
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    cfg = S.CONFIGS[3].with_size(WIDTH, HEIGHT)
+    with ShadingContext(0) as sc:
+        sc.set_pass(S.scene_pass(cfg))
+        sc.set_env_map(S.env_map())
+        whole = sc.shade(S.build_gbuffer(cfg, gpu)).cpu().numpy()
+    assert frame.shape == whole.shape
+    assert np.array_equal(frame.view(np.uint32), whole.view(np.uint32))
+
+
+def test_bench_multi_rank_rehearsal(gpu):
+    """bench.py at N = 4 (gloo, the one GPU shared): one JSON line from rank 0 with the gathered bands'
+    checksums matching and the per-rank band geometry of config 5."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "4", "--steps", "3", "--warmup", "1", "--ramp-ms", "0", "--dist-backend", "gloo",
+           "--rows-per-rank", "64"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env={**os.environ, "OMP_NUM_THREADS": "2"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = lines[0]
+    assert d["n_gpus"] == 4 and d["scaling"] == "weak"
+    assert d["gather_checksums_match"] is True
+    assert d["config"]["workload"].startswith("cfg5_8192x8192_64pt_ibl_rowbands")
+    assert d["config"]["rows_per_rank"] == 64 and d["config"]["width"] == 8192
+    assert d["value"] > 0 and d["cpu_baseline"] is None
