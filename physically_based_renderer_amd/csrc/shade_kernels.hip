@@ -7,15 +7,14 @@
 // (pbr_device_math_x2.h): every light-loop operation except the transcendental seeds and compares
 // issues once for both pixels.
 //
-// The light list is staged through LDS in chunks of 256 lights (3 float4 per light = the reference's
-// 48-byte `Light`, LightingUtil.hlsl:9-17); every lane reads the same LDS record (broadcast).
-//
-// Tiled culling (PBR_FLAG_TILED_CULLING): the tile's world-space AABB comes from wave64 min/max
-// shuffles plus a 4-entry LDS combine; each chunk's point/spot lights are range-tested against it,
-// one light per work-item, and compacted IN ORDER into LDS with a 64-bit ballot + mbcnt prefix. A
-// light is dropped only when it is provably beyond the 100-unit range of every pixel of the tile, so
-// the reference loop (LightingUtil.hlsl:131) would have added +0 for it: the culled result is
-// bit-identical to the unculled one.
+// Lights: the pair kernel reads each light record (3 float4 = the reference's 48-byte `Light`,
+// LightingUtil.hlsl:9-17) with wave-uniform scalar loads; nothing is staged and the light loop has no
+// barrier. Tiled culling (PBR_FLAG_TILED_CULLING) is per wave: the wave's 64x2-pixel world-space box
+// (wave64 butterflies), one range test per lane and light, and the ballot of the survivors walked in
+// order. A light is dropped only when it is provably beyond the 100-unit range of every pixel of the
+// wave, so the reference loop (LightingUtil.hlsl:131) would have added +0 for it: the culled result
+// is bit-identical to the unculled one. (The one-pixel kernel below stages lights through LDS and
+// culls per workgroup, with an in-order ballot + mbcnt compaction.)
 //
 // Exact fallback: a pixel whose inputs or intermediates leave the fast-path window for any light is
 // flagged; after the fast loop, a block with any flagged pixel re-runs the light loop for those
@@ -33,9 +32,6 @@ namespace pbr {
 namespace {
 
 constexpr int kTileW = 64;  // pixels; 32 work-items x 2 pixels
-#ifndef PBR_X2_LIGHT_UNROLL
-#define PBR_X2_LIGHT_UNROLL 1
-#endif
 #ifndef PBR_X2_MIN_WAVES
 #define PBR_X2_MIN_WAVES 4  // waves per SIMD the packed kernel is register-allocated for
 #endif
