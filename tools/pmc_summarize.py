@@ -4,7 +4,7 @@ that bench.py reads for roofline.traffic.
 
 HBM bytes per launch = FETCH_SIZE x 2 + WRITE_SIZE (KiB; gfx950 FETCH_SIZE reports half of a
 coalesced read, MI355X_MICROARCH.md "HBM"), averaged over the shading kernel's dispatches.
-usage: python tools/pmc_summarize.py <tag> <workload> <pixels> <bytes_per_px> <lights> <revision>
+usage: python tools/pmc_summarize.py <tag> <workload> <pixels> <bytes_per_px> <lights> <revision> [<profiles subdir>]
 """
 import csv
 import glob
@@ -38,7 +38,8 @@ def main():
     tag, workload, pixels, bpp, lights, revision = sys.argv[1:7]
     pixels, bpp, lights = int(pixels), int(bpp), int(lights)
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    dst = os.path.join(ROOT, "profiles", tag)
+    dst_tag = sys.argv[7] if len(sys.argv) > 7 else tag
+    dst = os.path.join(ROOT, "profiles", dst_tag)
     os.makedirs(dst, exist_ok=True)
     shutil.copy(find(f"{src}/kt/**/*kernel_stats.csv"), os.path.join(dst, f"kernel_stats_{workload}.csv"))
     shutil.copy(os.path.join(src, "kt.log"), os.path.join(dst, f"bench_{workload}.log"))
@@ -62,7 +63,7 @@ def main():
         # SQ_ACTIVE_INST_VALU counts quad-cycles summed over waves; GRBM_GUI_ACTIVE is summed over the 8
         # XCDs (MI355X_MICROARCH.md): VALU-issue cycles per SIMD over kernel cycles.
         "valu_issue_busy": counters["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / (counters["GRBM_GUI_ACTIVE"] / 8),
-        "source": f"profiles/{tag}/pmc_*_{workload}.csv (rocprofv3 --pmc, separate passes, bench.py --steps 5)",
+        "source": f"profiles/{dst_tag}/pmc_*_{workload}.csv (rocprofv3 --pmc, separate passes, bench.py --steps 5)",
         "kernel_revision": revision,
     }
     # Kernel trace of the bench run itself: mean launch time over the timed steps (the last K launches;
