@@ -274,13 +274,26 @@ def adversarial_planes(rng, h, w):
     return p
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(8))
 def test_fast_path_is_bit_identical_to_exact_only(seed, shading_ctx, gpu, env_map):
     """The exact fast division/sqrt path must reproduce the compiler's IEEE sequences bit for bit,
-    on ordinary and adversarial inputs, for every light type and both ambient modes."""
+    on ordinary and adversarial inputs, for every light type and both ambient modes. Seeds 6-7: scene
+    G-buffers (waves on the lean loop) lit by lights outside the per-light window (flag set by
+    pbr_set_pass), which must send their pixels to the exact re-pass."""
     rng = np.random.default_rng(100 + seed)
     h, w = 64, 256
-    if seed < 2:
+    if seed >= 6:
+        cfg = S.CONFIGS[[3, 4][seed - 6]].with_size(w, h)
+        p, _ = S.fill_gbuffer_host(cfg)
+        L = S.scene_pass(cfg).light_array()[:40].copy()
+        nd, npt, ns = 4, 30, 6
+        L[:nd, 4:7] = rng.normal(size=(nd, 3))
+        L[1, 4:7] = (1e-30, 0.5, 0.0)  # directional: a component below 2^-20
+        L[2, 4:7] = (20.0, -1.0, 0.0)  # above 16
+        L[nd + 3, 8:11] = (2.0 ** 21, 0.0, 1.0)  # point: beyond 2^20
+        L[nd + 7, 8:11] = (1e-40, 3.0, 2.0)  # subnormal component
+        L[nd + npt + 1, 8:11] = (2.0 ** -25, 1.0, 1.0)
+    elif seed < 2:
         cfg = S.CONFIGS[[3, 4][seed]].with_size(w, h)
         p, _ = S.fill_gbuffer_host(cfg)
         pc = S.scene_pass(cfg)
