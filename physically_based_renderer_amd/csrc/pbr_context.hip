@@ -183,7 +183,8 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
         std::memcpy(ctx->h_ring[slot], pass->lights, sizeof(pbr_light) * (size_t)n);
         // The kernel's per-light fast-path flag travels in the unused pad1 of the uploaded copy
         // (the caller's array is not touched): directional L = -Direction components, point / spot
-        // positions, each 0 or |x| in [2^-20, 16] / [2^-20, 2^20] (pbr_device_math.h, light_window_ok).
+        // positions, each 0 or |x| in [2^-20, 16] / [2^-20, 2^20] (pbr_device_math.h, light_window_ok),
+        // and a finite point / spot strength.
         for (long long i = 0; i < n; ++i) {
             pbr_light& L = ctx->h_ring[slot][i];
             const bool directional = i < nd;
@@ -193,6 +194,9 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
             for (int k = 0; k < 3; ++k) {
                 const float a = std::fabs(c[k]);
                 ok = ok && (a == 0.0f || (a >= 0x1p-20f && a <= hi));
+                // point / spot: a finite strength, so that an out-of-range lane's zero-attenuated
+                // contribution is +-0 (pbr_device_math_x2.h, point_or_spot_x2)
+                if (!directional) ok = ok && std::isfinite(L.strength[k]);
             }
             L.pad1 = ok ? 1.0f : 0.0f;
         }

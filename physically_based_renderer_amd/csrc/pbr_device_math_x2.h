@@ -175,8 +175,17 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance
     v2 ndf_g = ndf * g;
     v2 denom = q.four_n_dot_v * n_dot_l + 0.001f;
     f3x2 nom = f3x2{ndf_g * f.x, ndf_g * f.y, ndf_g * f.z};
-    ok &= eq(ndf_g, 0.0f) | in_win(ndf_g, 0x1p-30f, 0x1p40f);
-    if (!LEAN) ok &= q.f0_nonzero | eq(p, 0.0f) | ge(p, 0x1p-40f);
+    if (LEAN) {
+        // ndf_g is +-0 or positive here (a^2 > 0, den > 0, N.L and ggx_v >= 0) and at most 2^38
+        // (ndf <= a^2 / 2^-37 <= 2^37; ggx_l, ggx_v <= 1 + 2^-19 for |N.L|, |N.V| <= 1 + 2^-19), so the
+        // window is "0 or >= 2^-30": one integer op and one compare on the bit pattern, b - 1 >= bits(2^-30) - 1
+        // (unsigned; +0 wraps to the maximum, -0 is 0x80000000 and passes too).
+        const uint32_t bx = __builtin_bit_cast(uint32_t, ndf_g.x) - 1u, by = __builtin_bit_cast(uint32_t, ndf_g.y) - 1u;
+        ok &= mask2(bx >= 0x30800000u - 1u, by >= 0x30800000u - 1u);
+    } else {
+        ok &= eq(ndf_g, 0.0f) | in_win(ndf_g, 0x1p-30f, 0x1p40f);
+        ok &= q.f0_nonzero | eq(p, 0.0f) | ge(p, 0x1p-40f);
+    }
     const Recip2 rd = recip_nr(denom);
     f3x2 spec = f3x2{div_nr(nom.x, rd), div_nr(nom.y, rd), div_nr(nom.z, rd)};
     f3x2 kd = f3x2{(1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal};
@@ -200,8 +209,23 @@ __device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, float4
     return brdf_x2<LEAN>(q, splat3(s.x, s.y, s.z), l, h, ok);
 }
 
+// max(x, 0.01f) of CalcAttenuation (LightingUtil.hlsl:38) as one v_med3_f32(x, 0.01, 2^100): the
+// same value as maxNum for every x <= 2^100 (an in-window distance is below 2^22), without the
+// quieting v_max the compiler puts in front of an IEEE-mode v_max_f32 whose input it cannot prove
+// canonical (with +inf as the bound the intrinsic is folded back into that maxnum). A NaN or huge
+// distance fails the window (ge(dist, 2^-20) / the position windows), so that lane is redone on the
+// exact path whatever this returns.
+__device__ __forceinline__ v2 max_dsat(v2 dist) {
+    return v2{__builtin_amdgcn_fmed3f(dist.x, 0.01f, 0x1p100f),
+              __builtin_amdgcn_fmed3f(dist.y, 0.01f, 0x1p100f)};
+}
+
 // ComputePointLight / ComputeSpotLight, packed fast path. `lit` = the range test passed (exact,
-// as in the scalar version). Lanes with lit == 0 carry garbage in `out` and are never added.
+// as in the scalar version). For a lane with lit == 0 the attenuation is set to +0, so the returned
+// contribution is (finite) * 0 = +-0 whenever the lane is inside the window (`ok`: every value of the
+// fast path is then finite; pbr_set_pass clears the light's window flag when its strength is not
+// finite), and adding +-0 to the running sum is the identity the reference's skipped light is. Lanes
+// outside the window are redone by the caller whether lit or not.
 template <bool SPOT, bool LEAN>
 __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const f3x2& pos,
                                                  float4 s, float4 d, float4 p, m2& lit, m2& ok) {
@@ -212,12 +236,13 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
     const Recip2 rdist = recip_nr(dist);
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     f3x2 h = normalize_x2(add3(q.v, l), ok);
-    v2 dsat = vmax(dist, splat(0.01f));
+    v2 dsat = max_dsat(dist);
     v2 att = recip_nr(dsat * dsat).r;  // RN(1/y) already (see point_or_spot_light)
     if (SPOT) {
         v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
+    att = vsel(lit, att, splat(0.0f));
     return brdf_x2<LEAN>(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
 }
 

@@ -157,10 +157,11 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         m2 lit;
         const f3x2 c = kind == 1 ? point_or_spot_x2<false, LEAN>(q, pos, r.s, r.d, r.p, lit, ok)
                                  : point_or_spot_x2<true, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
-        redo |= lit & ~ok;
-        // An unlit light adds +0 in the reference (identity on a sum that is never -0).
-        direct = add3(direct, f3x2{vsel(lit, c.x, splat(0.0f)), vsel(lit, c.y, splat(0.0f)),
-                                   vsel(lit, c.z, splat(0.0f))});
+        (void)lit;
+        // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation) when
+        // inside the window, and every lane outside it is redone.
+        redo |= ~ok;
+        direct = add3(direct, c);
     };
 #pragma unroll 1
     for (int kind = 1; kind <= 2; ++kind) {
