@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBR_ABI_VERSION 2
+#define PBR_ABI_VERSION 3
 #define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
 
 typedef enum pbr_status {
@@ -159,12 +159,29 @@ int pbr_set_sky_map_f32(pbr_context* ctx, const float* texels, int32_t width, in
  * format conversion are fused into the shading kernel). Asynchronous on `stream`. */
 int pbr_shade_frame(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* frame, void* stream);
 
-/* Tiled-culling statistics of the last culled pass on `stream` (synchronises that stream):
+/* Tiled-culling statistics of the last pass on `stream` (synchronises that stream), zeros when that
+ * pass did not cull:
  * total surviving point/spot lights summed over the culling tiles that hold geometry, and the number
  * of those tiles. A culling tile is one wave64's pixels (64x2 in the default pixel-pair layout, 32x8
  * workgroups in the one-pixel layout). The kernel writes per-workgroup counts (no atomics); this
  * call sums them on the host. */
 int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream);
+
+/* Statistics of the last shading pass of the context (new; the reference has no counterpart). */
+typedef struct pbr_pass_stats {
+    int64_t workgroups;       /* workgroups of the pass (64x8-pixel tiles; 32x8 in the one-pixel layout) */
+    int64_t culled;           /* 1 when the pass ran tiled culling, else 0 */
+    int64_t cull_tiles;       /* culling tiles with geometry (0 without culling) */
+    int64_t cull_tile_lights; /* surviving point/spot lights summed over those tiles (0 without culling) */
+    int64_t exact_pixels;     /* geometry pixels whose light sum the exact path re-evaluated (inputs or
+                                 intermediates outside the fast-path window; every geometry pixel with
+                                 PBR_FLAG_EXACT_ONLY) */
+} pbr_pass_stats;
+
+/* Fill *out with the statistics of the last pbr_shade_gbuffer / pbr_shade_frame call (synchronises
+ * `stream`, which must be the stream that pass ran on or one ordered after it). All zero before the
+ * first pass. The kernel writes one record per workgroup; this call sums them on the host. */
+int pbr_last_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream);
 
 /* ---- Host G-buffer fill (replaces the VS + rasteriser front-end, Default.hlsl:22-45) ---------- */
 

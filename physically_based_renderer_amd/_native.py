@@ -122,6 +122,17 @@ class Camera(ctypes.Structure):
     ]
 
 
+class PassStats(ctypes.Structure):
+    """pbr_pass_stats: statistics of the last shading pass."""
+    _fields_ = [
+        ("workgroups", ctypes.c_int64),
+        ("culled", ctypes.c_int64),
+        ("cull_tiles", ctypes.c_int64),
+        ("cull_tile_lights", ctypes.c_int64),
+        ("exact_pixels", ctypes.c_int64),
+    ]
+
+
 class SceneDesc(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32),
@@ -152,6 +163,7 @@ SIGNATURES = {
                                        ctypes.c_void_p]),
     "pbr_last_cull_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "pbr_last_pass_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(PassStats), ctypes.c_void_p]),
     "pbr_gbuffer_fill": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,
                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int32]),
     "pbr_gbuffer_fill_coverage": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,
@@ -182,6 +194,8 @@ def lib() -> ctypes.CDLL:
             raise ImportError(f"{LIB_PATH} not built: run `make -C {CSRC_DIR}` or __graft_entry__.build()")
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if "PBR_LIB_PATH" in os.environ and not hasattr(handle, name):
+                continue  # development A/B against an older build: bind what it exports
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

@@ -38,11 +38,13 @@ struct pbr_context {
     int ambient_mode = 0;
     uint32_t flags = 0;
     bool pass_set = false;
-    // Tiled-culling statistics of the last culled pass: one int32 per tile (surviving lights, -1 = no
-    // geometry), summed on the host by pbr_last_cull_stats.
+    // Statistics of the last pass: one record of pbr::kStatsPerBlock int32 per workgroup ([surviving
+    // point/spot lights summed over its culling tiles, culling tiles with geometry, pixels redone by the
+    // exact path]), summed on the host by pbr_last_pass_stats / pbr_last_cull_stats.
     int32_t* d_tile_kept = nullptr;
     int64_t tile_kept_capacity = 0;
-    int64_t last_cull_tiles = 0;
+    int64_t last_tiles = 0;
+    bool last_culled = false;
     int pixels_per_thread = 2;  // kernel layout: packed pixel pairs (measured faster); PBR_PIXELS_PER_THREAD=1 overrides
     std::string last_error;
     std::mutex mu;
@@ -331,23 +333,24 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     if (!g.ok) return PBR_ERR_NO_DEVICE;
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
-    if (cull) {
+    {
         const int64_t tiles = pbr::shade_tile_count(gb->width, gb->height, a.pixels_per_thread);
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (tiles > ctx->tile_kept_capacity) {
             // Growing: the old buffer may still be written by queued kernels on any stream.
             if (ctx->d_tile_kept) {
                 e = hipDeviceSynchronize();
-                if (e != hipSuccess) return fail_hip(ctx, e, "cull stats sync");
+                if (e != hipSuccess) return fail_hip(ctx, e, "pass stats sync");
                 (void)hipFree(ctx->d_tile_kept);
                 ctx->d_tile_kept = nullptr;
                 ctx->tile_kept_capacity = 0;
             }
-            e = hipMalloc(&ctx->d_tile_kept, 2 * sizeof(int32_t) * (size_t)tiles);
-            if (e != hipSuccess) return fail_hip(ctx, e, "cull stats hipMalloc");
+            e = hipMalloc(&ctx->d_tile_kept, pbr::kStatsPerBlock * sizeof(int32_t) * (size_t)tiles);
+            if (e != hipSuccess) return fail_hip(ctx, e, "pass stats hipMalloc");
             ctx->tile_kept_capacity = tiles;
         }
-        ctx->last_cull_tiles = tiles;
+        ctx->last_tiles = tiles;
+        ctx->last_culled = cull;
         a.tile_kept = ctx->d_tile_kept;
     }
     e = pbr::launch_shade(a, s);
@@ -392,24 +395,51 @@ int pbr_shade_frame(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame
     return shade(ctx, gb, frame, stream);
 }
 
-int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream) {
-    if (!ctx || !sum_tile_lights || !num_tiles) return PBR_ERR_INVALID_ARGUMENT;
+}  // extern "C"
+
+namespace {
+
+// Sum the per-workgroup records of the last pass.
+int sum_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream, const char* what) {
+    *out = pbr_pass_stats{};
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;
-    *sum_tile_lights = 0;
-    *num_tiles = 0;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (ctx->last_cull_tiles == 0) return PBR_OK;  // no culled pass yet
-    std::vector<int32_t> h(2 * (size_t)ctx->last_cull_tiles);
+    if (ctx->last_tiles == 0) return PBR_OK;  // no pass yet (or an empty frame)
+    std::vector<int32_t> h(pbr::kStatsPerBlock * (size_t)ctx->last_tiles);
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e = hipMemcpyAsync(h.data(), ctx->d_tile_kept, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return fail_hip(ctx, e, "pbr_last_cull_stats");
-    for (size_t t = 0; t < h.size(); t += 2) {  // [survivors, culling units with geometry] per workgroup
-        *sum_tile_lights += h[t];
-        *num_tiles += h[t + 1];
+    if (e != hipSuccess) return fail_hip(ctx, e, what);
+    out->workgroups = ctx->last_tiles;
+    out->culled = ctx->last_culled ? 1 : 0;
+    for (size_t t = 0; t < h.size(); t += pbr::kStatsPerBlock) {
+        out->cull_tile_lights += h[t];
+        out->cull_tiles += h[t + 1];
+        out->exact_pixels += h[t + 2];
     }
     return PBR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num_tiles, void* stream) {
+    if (!ctx || !sum_tile_lights || !num_tiles) return PBR_ERR_INVALID_ARGUMENT;
+    *sum_tile_lights = 0;
+    *num_tiles = 0;
+    pbr_pass_stats st;
+    const int rc = sum_pass_stats(ctx, &st, stream, "pbr_last_cull_stats");
+    if (rc != PBR_OK) return rc;
+    *sum_tile_lights = st.cull_tile_lights;
+    *num_tiles = st.cull_tiles;
+    return PBR_OK;
+}
+
+int pbr_last_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream) {
+    if (!ctx || !out) return PBR_ERR_INVALID_ARGUMENT;
+    return sum_pass_stats(ctx, out, stream, "pbr_last_pass_stats");
 }
 
 }  // extern "C"

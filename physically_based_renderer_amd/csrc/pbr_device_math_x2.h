@@ -180,7 +180,9 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance
         // (ndf <= a^2 / 2^-37 <= 2^37; ggx_l, ggx_v <= 1 + 2^-19 for |N.L|, |N.V| <= 1 + 2^-19), so the
         // window is "0 or >= 2^-30": one integer op and one compare on the bit pattern, b - 1 >= bits(2^-30) - 1
         // (unsigned; +0 wraps to the maximum, -0 is 0x80000000 and passes too).
-        const uint32_t bx = __builtin_bit_cast(uint32_t, ndf_g.x) - 1u, by = __builtin_bit_cast(uint32_t, ndf_g.y) - 1u;
+        // Element bits through __float_as_uint (a by-value copy): this clang reads element 0 for
+        // __builtin_bit_cast(uint32_t, v.y) on an ext_vector_type element (compiler notes).
+        const uint32_t bx = __float_as_uint(ndf_g.x) - 1u, by = __float_as_uint(ndf_g.y) - 1u;
         ok &= mask2(bx >= 0x30800000u - 1u, by >= 0x30800000u - 1u);
     } else {
         ok &= eq(ndf_g, 0.0f) | in_win(ndf_g, 0x1p-30f, 0x1p40f);

@@ -43,16 +43,19 @@ struct FrameArgs {
     const float4* sky;         // sky_w * sky_h RGBA fp32 (required when coverage != nullptr)
 };
 
+constexpr int kStatsPerBlock = 3;
+
 struct LaunchArgs {
     GBufferArgs gb;
     PassArgs ps;
     const float4* lights;  // 3 float4 per light (the reference's 48-byte Light)
     const float4* env;     // env_w * env_h RGBA fp32, or nullptr
     FrameArgs frame;
-    // CULL only: two ints per workgroup (blockIdx.y * gridDim.x + blockIdx.x): surviving point/spot
-    // lights summed over its culling units, and the number of culling units with geometry (the pair
-    // layout culls per wave = 64x2 pixels, the one-pixel layout per workgroup = 32x8). Plain stores:
-    // one same-address global atomic per tile serialised the whole grid (0.29 ms per 4K frame).
+    // kStatsPerBlock ints per workgroup (blockIdx.y * gridDim.x + blockIdx.x): surviving point/spot
+    // lights summed over its culling units and the number of culling units with geometry (both 0
+    // without CULL; the pair layout culls per wave = 64x2 pixels, the one-pixel layout per workgroup =
+    // 32x8), and the geometry pixels the exact path redid. Plain stores: one same-address global atomic
+    // per tile serialised the whole grid (0.29 ms per 4K frame). May be nullptr.
     int32_t* tile_kept;
     int ambient_mode;
     bool f0_plane, apply_ao, cull;

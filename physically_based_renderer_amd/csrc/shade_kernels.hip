@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "pbr_device_math.h"
 #include "pbr_device_math_x2.h"
@@ -62,6 +63,7 @@ struct Lds {
     int wave_cnt[kBlock / 64];
     float bounds[kBlock / 64][6];
     int kept_sum, geo_waves;  // tiled-culling statistics of the block
+    int exact_px;             // pixels of the block the exact path redid
 };
 
 // Stage lights [begin, begin+count) of the global list into LDS, culled against the tile when CULL.
@@ -151,24 +153,23 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
     }
     const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
-    auto point = [&](int kind, int j) {
-        const LightRec r = light_rec(lights, j);
-        m2 ok = fast_ok & all2(r.p.w != 0.0f);
-        m2 lit;
-        const f3x2 c = kind == 1 ? point_or_spot_x2<false, LEAN>(q, pos, r.s, r.d, r.p, lit, ok)
-                                 : point_or_spot_x2<true, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
-        (void)lit;
-        // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation) when
-        // inside the window, and every lane outside it is redone.
-        redo |= ~ok;
-        direct = add3(direct, c);
-    };
-#pragma unroll 1
-    for (int kind = 1; kind <= 2; ++kind) {
-        const int b0 = kind == 1 ? pt_begin : sp_begin, b1 = kind == 1 ? sp_begin : end;
+    // Point lights, then spot lights: one loop each (SPOT is a template constant, so the point loop
+    // carries no spot code and no per-light branch on the kind).
+    auto run_kind = [&](auto spot_tag, int b0, int b1) {
+        constexpr bool SPOT = decltype(spot_tag)::value;
+        auto point = [&](int j) {
+            const LightRec r = light_rec(lights, j);
+            m2 ok = fast_ok & all2(r.p.w != 0.0f);
+            m2 lit;
+            const f3x2 c = point_or_spot_x2<SPOT, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
+            // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation)
+            // when inside the window, and every lane outside it is redone.
+            redo |= ~ok;
+            direct = add3(direct, c);
+        };
         if (!CULL) {
-            for (int j = b0; j < b1; ++j) point(kind, j);
-            continue;
+            for (int j = b0; j < b1; ++j) point(j);
+            return;
         }
         for (int base = b0; base < b1; base += 64) {
             const int j = base + (int)(threadIdx.x & 63);
@@ -185,10 +186,12 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
             while (m) {
                 const int jl = base + __builtin_ctzll(m);
                 m &= m - 1;
-                point(kind, jl);
+                point(jl);
             }
         }
-    }
+    };
+    run_kind(std::false_type{}, pt_begin, sp_begin);
+    if (end > sp_begin) run_kind(std::true_type{}, sp_begin, end);
     return direct;
 }
 
@@ -362,7 +365,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                             bool exact_only) {
     __shared__ Lds s;
     load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
-    if (threadIdx.x == 0) s.kept_sum = s.geo_waves = 0;
+    if (threadIdx.x == 0) s.kept_sum = s.geo_waves = s.exact_px = 0;
     __syncthreads();
 
     const int tid = threadIdx.x;
@@ -442,6 +445,10 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
     f3 da = lane(d2, 0), db = lane(d2, 1);
     const bool need_a = ga && on(redo.x), need_b = gb_ && on(redo.y);
+    {  // statistics: pixels this wave sends to the exact path (scalar popcounts; LDS add only if any)
+        const int n = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
+        if (n != 0 && (tid & 63) == 0) atomicAdd(&s.exact_px, n);
+    }
     if (__syncthreads_or(need_a || need_b)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
         f3 ea, eb;
         lighting_exact<false>(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, s, TileBounds{},
@@ -449,10 +456,11 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         if (need_a) da = ea;
         if (need_b) db = eb;
     }
-    if (CULL && tid == 0 && tile_kept != nullptr) {  // after the barrier above: every wave has added
+    if (tid == 0 && tile_kept != nullptr) {  // after the barrier above: every wave has added
         const int64_t t = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-        tile_kept[2 * t] = s.kept_sum;
-        tile_kept[2 * t + 1] = s.geo_waves;
+        tile_kept[kStatsPerBlock * t] = CULL ? s.kept_sum : 0;
+        tile_kept[kStatsPerBlock * t + 1] = CULL ? s.geo_waves : 0;
+        tile_kept[kStatsPerBlock * t + 2] = s.exact_px;
     }
 
     const int64_t orow = (int64_t)y * fr.out_stride;
@@ -582,15 +590,17 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
     f3 direct = mk3(0.0f, 0.0f, 0.0f);
     if (any_geometry) direct = lighting_fast1<CULL>(q, pos, lights, ps, s, tb, cull_enabled, redo, kept_total);
     const bool need = geom && redo;
-    if (__syncthreads_or(need)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
+    const int n_exact = __syncthreads_count(need);
+    if (n_exact != 0) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
         f3 e, unused;
         lighting_exact<CULL>(q, q, pos, pos, need, false, lights, ps, s, tb, cull_enabled, e, unused);
         if (need) direct = e;
     }
-    if (CULL && tid == 0 && tile_kept != nullptr) {  // this layout culls per block (32x8 pixels)
+    if (tid == 0 && tile_kept != nullptr) {  // this layout culls per block (32x8 pixels)
         const int64_t t = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-        tile_kept[2 * t] = any_geometry ? kept_total : 0;
-        tile_kept[2 * t + 1] = any_geometry ? 1 : 0;
+        tile_kept[kStatsPerBlock * t] = CULL && any_geometry ? kept_total : 0;
+        tile_kept[kStatsPerBlock * t + 1] = CULL && any_geometry ? 1 : 0;
+        tile_kept[kStatsPerBlock * t + 2] = n_exact;
     }
     if (valid)
         store_pixel(fr, (int64_t)y * fr.out_stride + x,

@@ -259,8 +259,16 @@ class ShadingContext:
                                          ctypes.c_void_p(_stream_handle(stream))), "pbr_shade_frame", self._h)
         return out
 
+    def pass_stats(self, stream=None) -> dict:
+        """pbr_last_pass_stats of the last pass as a dict (workgroups, culled, cull_tiles,
+        cull_tile_lights, exact_pixels)."""
+        st = N.PassStats()
+        N.check(self.lib.pbr_last_pass_stats(self._h, ctypes.byref(st), ctypes.c_void_p(_stream_handle(stream))),
+                "pbr_last_pass_stats", self._h)
+        return {name: getattr(st, name) for name, _ in N.PassStats._fields_}
+
     def cull_stats(self, stream=None):
-        """(sum of surviving point/spot lights over tiles, tiles) of the last culled pass."""
+        """(sum of surviving point/spot lights over tiles, tiles) of the last pass ((0, 0) unless it culled)."""
         s, t = ctypes.c_int64(), ctypes.c_int64()
         N.check(self.lib.pbr_last_cull_stats(self._h, ctypes.byref(s), ctypes.byref(t),
                                              ctypes.c_void_p(_stream_handle(stream))), "pbr_last_cull_stats", self._h)

@@ -19,7 +19,7 @@ def test_library_loads_and_exports_every_header_symbol():
         assert hasattr(lib, name), f"{name} declared in pbr_shade.h but not exported"
         assert name in N.SIGNATURES, f"{name} has no ctypes signature"
     assert set(N.SIGNATURES) == set(declared)
-    assert lib.pbr_abi_version() == 2
+    assert lib.pbr_abi_version() == 3
 
 
 def test_exports_are_c_symbols():
@@ -39,7 +39,7 @@ def test_library_is_built_for_gfx950():
 STRUCTS = {  # C struct -> ctypes mirror
     "pbr_light": "Light", "pbr_pass_desc": "PassDesc", "pbr_gbuffer_soa": "GBufferSoA",
     "pbr_frame_desc": "FrameDesc", "pbr_scene_assets": "SceneAssets", "pbr_camera": "Camera",
-    "pbr_scene_desc": "SceneDesc",
+    "pbr_scene_desc": "SceneDesc", "pbr_pass_stats": "PassStats",
 }
 
 
@@ -85,6 +85,7 @@ def test_null_arguments_are_rejected_without_a_device():
     assert lib.pbr_set_env_map(None, None, 0, 0, None) == -1
     assert lib.pbr_shade_gbuffer(None, None, None, 0, None) == -1
     assert lib.pbr_last_cull_stats(None, None, None, None) == -1
+    assert lib.pbr_last_pass_stats(None, None, None) == -1
     assert lib.pbr_gbuffer_fill(None, 0, 0, None, 0, 1) == -1
     assert lib.pbr_scene_pass(None, 0, None, None) == -1
 
