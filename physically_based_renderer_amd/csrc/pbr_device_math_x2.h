@@ -52,6 +52,17 @@ __device__ __forceinline__ v2 splat(float s) { return (v2)(s); }
 __device__ __forceinline__ f3x2 splat3(float x, float y, float z) { return f3x2{splat(x), splat(y), splat(z)}; }
 __device__ __forceinline__ f3 lane(const f3x2& v, int i) { return i ? mk3(v.x.y, v.y.y, v.z.y) : mk3(v.x.x, v.y.x, v.z.x); }
 
+// saturate(dot(a, b)) with the saturate folded into the dot's last packed add as its clamp bit
+// (v_pk_add_f32 ... clamp: the IEEE sum, then clamped to [0, 1]; DX10_CLAMP maps NaN to 0, as HLSL's
+// saturate does). The compiler applies the clamp as a separate v_max per element. Inline asm: the
+// s_nop 1 pads keep two wait states on both sides, whatever hazard the neighbours would need.
+__device__ __forceinline__ v2 dot3_sat(f3x2 a, f3x2 b) {
+    const v2 t = a.x * b.x + a.y * b.y, u = a.z * b.z;
+    v2 r;
+    asm("s_nop 1\n\tv_pk_add_f32 %0, %1, %2 clamp\n\ts_nop 1" : "=v"(r) : "v"(t), "v"(u));
+    return r;
+}
+
 struct Recip2 {
     v2 y, r;
 };
@@ -169,7 +180,7 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance
     v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
     v2 ggx_l = div_nr(n_dot_l, recip_nr(n_dot_l * q.one_minus_k + q.k));
     v2 g = ggx_l * q.ggx_v;
-    v2 cos_theta = vsat(dot3(h, q.v));
+    v2 cos_theta = dot3_sat(h, q.v);
     v2 p = pow5_light(1.0f - cos_theta);
     f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
     v2 ndf_g = ndf * g;

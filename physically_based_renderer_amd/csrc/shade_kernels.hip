@@ -128,6 +128,12 @@ struct LightRec {
 __device__ __forceinline__ LightRec light_rec(const float4* __restrict__ lights, int j) {
     return LightRec{lights[3 * j], lights[3 * j + 1], lights[3 * j + 2]};
 }
+// The light's fast-path window flag (pbr_set_pass writes 1.0f or 0.0f into pad1) as a lane mask, on
+// the scalar unit: the record is in SGPRs, so an integer test of its bits needs no VALU compare.
+__device__ __forceinline__ m2 light_flag(const LightRec& r) {
+    const uint64_t m = (__float_as_uint(r.p.w) << 1) != 0u ? ~0ull : 0ull;
+    return m2{m, m};
+}
 __device__ __forceinline__ float uniform_f(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
 }
@@ -147,7 +153,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     for (int j = 0; j < ps.n_dir; ++j) {  // directional: never culled
         const LightRec r = light_rec(lights, j);
-        m2 ok = fast_ok & all2(r.p.w != 0.0f);
+        m2 ok = fast_ok & light_flag(r);
         const f3x2 c = directional_x2<LEAN>(q, r.s, r.d, ok);
         redo |= ~ok;
         direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
@@ -159,7 +165,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         constexpr bool SPOT = decltype(spot_tag)::value;
         auto point = [&](int j) {
             const LightRec r = light_rec(lights, j);
-            m2 ok = fast_ok & all2(r.p.w != 0.0f);
+            m2 ok = fast_ok & light_flag(r);
             m2 lit;
             const f3x2 c = point_or_spot_x2<SPOT, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
             // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation)
