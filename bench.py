@@ -113,8 +113,17 @@ def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int):
     got = gpu_frame[::step]
     err = O.rel_err(got, ref)
     exact = float(O.bit_equal(got, ref).mean())
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {
         "value": round(px / dt / 1e6, 4), "unit": "Mpix/s", "cores": n_threads, "kind": "port",
+        "cpu_model": model,
         "single_thread_value": round(st, 4),
         "sample": (f"every {step}th row of" if step > 1 else "all rows of") +
                   f" the same {cfg.width}x{cfg.height} frame ({px} px, {dt:.2f} s wall), "
