@@ -8,7 +8,8 @@ one step = one shading pass over the whole frame (inputs resident in HBM before 
 N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL): BASELINE config 5 geometry --
 an 8192-wide frame of 1024 rows per rank (8192x8192 at N = 8); one step = every rank shades its
 row band and the bands are gathered to rank 0 (pipelined: the gather of frame k overlaps the shading
-of frame k+1). Weak scaling: per-GPU work is fixed.
+of frame k+1) as the presented R8G8B8A8_UNORM frame (--output; shading is fp32 at every N). Weak
+scaling: per-GPU work is fixed.
 
 Rank 0 prints one JSON line ("Measurement"). The cpu_baseline leg times the CPU
 oracle (oracle/, test infrastructure) on a bounded row sample of the same frame and doubles as a
@@ -148,9 +149,11 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the benchmark); gloo = host-staged gather, for exercising the "
                          "multi-rank path on one GPU")
-    ap.add_argument("--output", default="rgba32f", choices=["rgba32f", "rgba8"],
-                    help="output format: fp32 RGBA (the metric's) or the reference's R8G8B8A8_UNORM back buffer "
-                         "(fused conversion; 4x smaller multi-GPU gather)")
+    ap.add_argument("--output", default="auto", choices=["auto", "rgba32f", "rgba8"],
+                    help="output format: fp32 RGBA or the reference's R8G8B8A8_UNORM back buffer (fused conversion, "
+                         "4x smaller multi-GPU gather). auto = rgba32f at N = 1 (the frame the parity check reads), "
+                         "rgba8 at N > 1 (the presented frame rank 0 assembles; an fp32 band is 134 MB per xGMI "
+                         "link per frame, longer than the band's shading, DESIGN.md section 7)")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="rows in the CPU-baseline sample (0 = the whole frame: ~1.5 s on 16 host threads)")
     args = ap.parse_args()
@@ -196,7 +199,8 @@ def main():
     log(f"rank {rank}/{world}: {workload} rows [{band.row_begin},{band.row_end}) fill {t_fill:.2f}s "
         f"upload {t_upload * 1e3:.1f} ms ({staging.numel() * 4 / t_upload / 1e9:.1f} GB/s H2D)")
 
-    rgba8 = args.output == "rgba8"
+    output = args.output if args.output != "auto" else ("rgba32f" if world == 1 else "rgba8")
+    rgba8 = output == "rgba8"
     out_dtype = torch.uint8 if rgba8 else torch.float32
     fmt = N.PBR_OUTPUT_RGBA8_UNORM if rgba8 else N.PBR_OUTPUT_RGBA32F
     outs = [torch.empty((band.rows_max, cfg.width, 4), dtype=out_dtype, device=device) for _ in range(2)]
@@ -341,7 +345,7 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "Mpix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "clock_ramp": {"ms": round(ramp_ms, 1), "launches": n_ramp},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "output": args.output,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "output": output,
             "data": "synthetic deterministic G-buffer (splitmix64 per pixel; rustediron metal/rough tiles; "
                     "Chelsea_Stairs 16-bit env)",
             "config": {"workload": workload, "width": cfg.width, "height": cfg.height,

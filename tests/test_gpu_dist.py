@@ -102,3 +102,4 @@ def test_bench_multi_rank_rehearsal(gpu):
     assert d["config"]["workload"].startswith("cfg5_8192x8192_64pt_ibl_rowbands")
     assert d["config"]["rows_per_rank"] == 64 and d["config"]["width"] == 8192
     assert d["value"] > 0 and d["cpu_baseline"] is None
+    assert d["output"] == "rgba8"  # N > 1 gathers the presented back-buffer format by default
