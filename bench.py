@@ -129,7 +129,38 @@ def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int):
         "sample": (f"every {step}th row of" if step > 1 else "all rows of") +
                   f" the same {cfg.width}x{cfg.height} frame ({px} px, {dt:.2f} s wall), "
                   f"oracle/pbr_oracle.c, -O2 -ffp-contract=off, {n_threads} pthreads",
-    }, float(err.max()), exact
+    }, float(err.max()), exact, (step, ref)
+
+
+def time_exact_mode(ctx, pc, gb, out, stream, args, fmt, rgba8, px):
+    """The same pass with PBR_FLAG_FAITHFUL cleared (correctly rounded, bit-identical to the oracle), timed
+    like the headline: warm-up, then K launches between synchronisations with HIP events around each.
+    Leaves the exact-mode frame in `out`."""
+    from physically_based_renderer_amd.renderer import PassConstants
+
+    ctx.set_pass(PassConstants(**{**pc.__dict__, "flags": int(pc.flags) & ~N.PBR_FLAG_FAITHFUL}))
+
+    def one():
+        if rgba8:
+            ctx.shade_frame(gb, out, fmt=fmt, stream=stream)
+        else:
+            ctx.shade(gb, out, stream)
+
+    for _ in range(max(args.warmup, 3)):
+        one()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        one()
+        b.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = [a.elapsed_time(b) for a, b in ev]
+    ctx.set_pass(pc)
+    return {"value": round(px * args.steps / wall / 1e6, 2), "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "avg_launch_ms": round(float(np.mean(ms)), 4), "median_launch_ms": round(float(np.median(ms)), 4)}
 
 
 def main():
@@ -154,6 +185,14 @@ def main():
                          "4x smaller multi-GPU gather). auto = rgba32f at N = 1 (the frame the parity check reads), "
                          "rgba8 at N > 1 (the presented frame rank 0 assembles; an fp32 band is 134 MB per xGMI "
                          "link per frame, longer than the band's shading, DESIGN.md section 7)")
+    ap.add_argument("--mode", default="faithful", choices=["exact", "faithful"],
+                    help="faithful (default) = PBR_FLAG_FAITHFUL: hardware reciprocals (<= 1 ulp; D3D allows 2.5 ulp "
+                         "for fp32 division) in the well-conditioned BRDF divisions, exact GGX/Fresnel chain, within "
+                         "the north-star 1e-5 (measured in the line: parity_max_rel); exact = correctly rounded "
+                         "reference semantics, bit-identical to the oracle.")
+    ap.add_argument("--exact-leg", action="store_true",
+                    help="N = 1, faithful mode: also time the exact mode on the same G-buffer and report it as exact_mode "
+                         "(off by default so that a kernel trace of the default command holds only the headline launches)")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="rows in the CPU-baseline sample (0 = the whole frame: ~1.5 s on 16 host threads)")
     args = ap.parse_args()
@@ -179,6 +218,8 @@ def main():
 
     t0 = time.perf_counter()
     pc = S.scene_pass(cfg)
+    if args.mode == "faithful":
+        pc.flags = int(pc.flags) | N.PBR_FLAG_FAITHFUL
     env = S.env_map() if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
     import torch as _t
     staging = _t.empty((N.NUM_PLANES, band.rows, cfg.width), dtype=_t.float32, pin_memory=True)
@@ -303,7 +344,7 @@ def main():
         band_px = cfg.width * band.rows
         bpp = bytes_per_pixel(pc, 4 if rgba8 else 16)
         achieved = bpp * band_px / avg_kernel_s / 1e9
-        traffic, valu_busy = load_pmc(workload)
+        traffic, valu_busy = load_pmc(workload + ("_faithful" if args.mode == "faithful" else ""))
         tile_px = 256 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 128  # culling unit: 32x8 / 64x2
         fpp = flops_per_pixel(pc, cull_note.get("lights_per_tile"), tile_px)
         tflops = fpp * band_px / avg_kernel_s / 1e12
@@ -331,10 +372,19 @@ def main():
         }
         cpu = None
         parity = {}
-        if world == 1 and not args.no_cpu_baseline and not rgba8:
-            frame = outs[0][: band.rows].cpu().numpy()
-            cpu, max_rel, exact = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows)
+        exact_leg = None
+        frame = outs[0][: band.rows].cpu().numpy() if world == 1 and not rgba8 else None
+        if world == 1 and args.mode == "faithful" and args.exact_leg:
+            exact_leg = time_exact_mode(ctx, pc, gb, outs[0], stream, args, fmt, rgba8, cfg.width * band.rows)
+        if frame is not None and not args.no_cpu_baseline:
+            cpu, max_rel, exact, (step, ref) = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows)
             parity = {"parity_max_rel": max_rel, "parity_bit_exact_frac": round(exact, 6)}
+            if exact_leg is not None:
+                from oracle import oracle as O  # test infrastructure: the checker only
+
+                got = outs[0][: band.rows].cpu().numpy()[::step]  # the exact-mode frame time_exact_mode left
+                exact_leg["parity_max_rel"] = float(O.rel_err(got, ref).max())
+                exact_leg["parity_bit_exact_frac"] = round(float(O.bit_equal(got, ref).mean()), 6)
         gather_note = {}
         if world > 1:
             gather_note = {"gather": ("batched isend/irecv star to rank 0 (RCCL), pipelined with the next frame"
@@ -345,7 +395,7 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "Mpix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "clock_ramp": {"ms": round(ramp_ms, 1), "launches": n_ramp},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "output": output,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "output": output, "mode": args.mode,
             "data": "synthetic deterministic G-buffer (splitmix64 per pixel; rustediron metal/rough tiles; "
                     "Chelsea_Stairs 16-bit env)",
             "config": {"workload": workload, "width": cfg.width, "height": cfg.height,
@@ -357,6 +407,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             **parity, **gather_note, **cull_note,
+            **({"exact_mode": exact_leg} if exact_leg is not None else {}),
             "pcie_h2d_gbps": round(staging.numel() * 4 / t_upload / 1e9, 2),
         }
         print(json.dumps(out), flush=True)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PBR_ABI_VERSION 3
+#define PBR_ABI_VERSION 4
 #define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
 
 typedef enum pbr_status {
@@ -63,8 +63,18 @@ enum pbr_pass_flags {
     PBR_FLAG_APPLY_AO = 1u << 1,    /* extension: ambient *= AO. The reference never reads its AO slot. */
     PBR_FLAG_TILED_CULLING = 1u << 2, /* per-tile range culling of point/spot lights; output is
                                          bit-identical to the unculled pass ("exact culling") */
-    PBR_FLAG_EXACT_ONLY = 1u << 3     /* validation mode: never take the exact fast division/sqrt path
+    PBR_FLAG_EXACT_ONLY = 1u << 3,    /* validation mode: never take the exact fast division/sqrt path
                                          ("exact fast path"); output is bit-identical, slower */
+    PBR_FLAG_FAITHFUL = 1u << 4       /* tolerance mode (ABI 4): the well-conditioned divisions of the BRDF
+                                         (NDF, Smith G1(N.L), specular denominator, diffuse / PI,
+                                         attenuation) use the hardware reciprocal (<= 1 ulp) instead of
+                                         correct rounding; the ill-conditioned GGX chain and Fresnel stay
+                                         exact. Output within 1e-5 relative of the reference evaluation
+                                         (the north-star bar; bound 4.6e-6, measured ~2e-7), not bit-identical.
+                                         Applies where every light term is >= 0 and the sum is short:
+                                         <= 64 lights, non-negative strengths, ambient and env texels
+                                         (checked on the host), albedo >= 0 and F0 in [0, 1] (checked per
+                                         wave); elsewhere the pass stays exact. */
 };
 
 /* Per-frame constants: the shading subset of cbPass (Core.hlsl:35-61, FrameResource.h:19-44) and

@@ -23,6 +23,7 @@ PBR_FLAG_F0_PLANE = 1 << 0
 PBR_FLAG_APPLY_AO = 1 << 1
 PBR_FLAG_TILED_CULLING = 1 << 2
 PBR_FLAG_EXACT_ONLY = 1 << 3
+PBR_FLAG_FAITHFUL = 1 << 4  # tolerance mode (pbr_shade.h): within 1e-5, not bit-identical
 PBR_OUTPUT_RGBA32F = 0
 PBR_OUTPUT_RGBA8_UNORM = 1
 PBR_SCENE_SPHERE_RUSTEDIRON = 1

@@ -31,6 +31,7 @@ struct pbr_context {
         uint16_t* d_u16 = nullptr;  // UNORM16 upload staging
         float4* d = nullptr;
         int w = 0, h = 0, capacity = 0;
+        bool nonneg = true;  // no negative or NaN texel (PBR_FLAG_FAITHFUL precondition for the IBL)
     };
     Texture env, sky;
     // Current pass.
@@ -38,6 +39,7 @@ struct pbr_context {
     int ambient_mode = 0;
     uint32_t flags = 0;
     bool pass_set = false;
+    bool faithful_pass_ok = false;  // light strengths and the constant ambient are finite and >= 0
     // Statistics of the last pass: one record of pbr::kStatsPerBlock int32 per workgroup ([surviving
     // point/spot lights summed over its culling tiles, culling tiles with geometry, pixels redone by the
     // exact path]), summed on the host by pbr_last_pass_stats / pbr_last_cull_stats.
@@ -152,7 +154,8 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
     if (n > PBR_MAX_LIGHTS) return PBR_ERR_INVALID_ARGUMENT;
     if (n > 0 && !pass->lights) return PBR_ERR_INVALID_ARGUMENT;
     if (!is_ambient_mode(pass->ambient_mode)) return PBR_ERR_INVALID_ARGUMENT;
-    const uint32_t known = PBR_FLAG_F0_PLANE | PBR_FLAG_APPLY_AO | PBR_FLAG_TILED_CULLING | PBR_FLAG_EXACT_ONLY;
+    const uint32_t known =
+        PBR_FLAG_F0_PLANE | PBR_FLAG_APPLY_AO | PBR_FLAG_TILED_CULLING | PBR_FLAG_EXACT_ONLY | PBR_FLAG_FAITHFUL;
     if (pass->flags & ~known) return PBR_ERR_INVALID_ARGUMENT;
 
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -223,6 +226,15 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
     p.n_dir = nd;
     p.n_point = np;
     p.n_spot = ns;
+    // PBR_FLAG_FAITHFUL's error bound needs every term of the light sum >= 0
+    // (pbr_device_math_x2.h, brdf_x2<true, true>): finite non-negative strengths and a non-negative
+    // constant ambient; and at most 64 lights, since the sum's rounding drift grows by <= 1 ulp per term.
+    bool nonneg = n <= 64;
+    for (long long i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) nonneg = nonneg && std::isfinite(pass->lights[i].strength[k]) && pass->lights[i].strength[k] >= 0.0f;
+    if (pass->ambient_mode == PBR_AMBIENT_CONSTANT)
+        for (int k = 0; k < 3; ++k) nonneg = nonneg && pass->ambient_light[k] >= 0.0f;
+    ctx->faithful_pass_ok = nonneg;
     ctx->ambient_mode = pass->ambient_mode;
     ctx->flags = pass->flags;
     ctx->pass_set = true;
@@ -272,6 +284,11 @@ int set_texture(pbr_context* ctx, pbr_context::Texture& t, const void* texels, b
     if (e != hipSuccess) return fail_hip(ctx, e, what);
     t.w = width;
     t.h = height;
+    t.nonneg = true;
+    if (!unorm16) {
+        const float* f = static_cast<const float*>(texels);
+        for (size_t i = 0; i < 4 * (size_t)n && t.nonneg; ++i) t.nonneg = f[i] >= 0.0f;  // false for NaN
+    }
     return PBR_OK;
 }
 
@@ -327,6 +344,8 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     a.apply_ao = apply_ao;
     a.cull = cull;
     a.exact_only = (ctx->flags & PBR_FLAG_EXACT_ONLY) != 0;
+    a.ps.faithful = (ctx->flags & PBR_FLAG_FAITHFUL) && !a.exact_only && ctx->faithful_pass_ok &&
+                    (ctx->ambient_mode != PBR_AMBIENT_IBL_DIFFUSE || ctx->env.nonneg);
     a.pixels_per_thread = ctx->pixels_per_thread;
 
     DeviceGuard g(ctx->device);

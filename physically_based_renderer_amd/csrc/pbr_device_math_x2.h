@@ -169,12 +169,42 @@ __device__ __forceinline__ v2 div_pi(v2 x) { return vfma(x, splat(kInvPiHi), x *
 //  * with |F0| in [2^-20, 1024] (per-pixel window, no zero component), F = F0 + (1 - F0) p is either
 //    near F0 or an exact cancellation (a multiple of ulp(F0)/2 >= 2^-45), so F is 0 or >= 2^-45 and
 //    ndf_g F stays inside the division window for any p: the p == 0 / p >= 2^-40 test is moot.
-template <bool LEAN>
+//
+// FAITHFUL (PBR_FLAG_FAITHFUL, lean waves only): the divisions whose operands are well conditioned --
+// the NDF's a^2 / den, GeometrySchlickGGX(N.L), the specular term's / denominator, kD * albedo / PI and
+// the attenuation -- take the hardware reciprocal (v_rcp_f32, <= 1 ulp) times the numerator instead of
+// the correctly rounded Markstein step, and the NDF*G window test goes away. Everything upstream of
+// the ill-conditioned GGX denominator (L, dist, H = normalize(V + L), N.H, den) and the Fresnel term
+// whose 1 - F cancels at grazing angles stay exact. Each light's contribution is then within ~16
+// roundings of the reference's, and with every term of the sum >= 0 (host: strengths, ambient, env >= 0,
+// <= 64 lights; kernel: albedo >= 0, F0 in [0, 1] per wave) the output stays within 4.6e-6 relative:
+// inside the north-star 1e-5 (tests/test_gpu_faithful.py). Not bit-identical; the
+// default mode is.
+__device__ __forceinline__ v2 rcp_hw(v2 y) { return v2{__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)}; }
+constexpr float kInvPi = 0x1.45f306p-2f;  // RN(1/kPi)
+
+template <bool LEAN, bool FAITHFUL = false>
 __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, m2& ok) {
+    static_assert(LEAN || !FAITHFUL, "FAITHFUL is a lean-wave variant");
     v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
     v2 n_dot_h_sqr = n_dot_h * n_dot_h;
     v2 den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
     den = kPi * den * den;
+    if (FAITHFUL) {
+        const v2 ndf = q.a_sqr * rcp_hw(den);
+        const v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
+        const v2 g = (n_dot_l * rcp_hw(n_dot_l * q.one_minus_k + q.k)) * q.ggx_v;
+        const v2 cos_theta = dot3_sat(h, q.v);
+        const v2 p = pow5_light(1.0f - cos_theta);
+        const f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
+        const v2 ndf_g = ndf * g;
+        const v2 rden = rcp_hw(q.four_n_dot_v * n_dot_l + 0.001f);
+        const f3x2 spec = f3x2{(ndf_g * f.x) * rden, (ndf_g * f.y) * rden, (ndf_g * f.z) * rden};
+        const f3x2 kd = f3x2{(1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal};
+        return f3x2{((((kd.x * q.albedo.x) * kInvPi) + spec.x) * radiance.x) * n_dot_l,
+                    ((((kd.y * q.albedo.y) * kInvPi) + spec.y) * radiance.y) * n_dot_l,
+                    ((((kd.z * q.albedo.z) * kInvPi) + spec.z) * radiance.z) * n_dot_l};
+    }
     if (!LEAN) ok &= ge(den, 0x1p-60f) & le(den, 0x1p60f);
     v2 ndf = div_nr(q.a_sqr, recip_nr(den));
     v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
@@ -215,11 +245,11 @@ __device__ __forceinline__ f3x2 normalize_x2(f3x2 v, m2& ok) {
 }
 
 // ComputeDirectionalLight, packed fast path.
-template <bool LEAN>
+template <bool LEAN, bool FAITHFUL = false>
 __device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, float4 s, float4 d, m2& ok) {
     f3x2 l = splat3(-d.x, -d.y, -d.z);
     f3x2 h = normalize_x2(add3(q.v, l), ok);
-    return brdf_x2<LEAN>(q, splat3(s.x, s.y, s.z), l, h, ok);
+    return brdf_x2<LEAN, FAITHFUL>(q, splat3(s.x, s.y, s.z), l, h, ok);
 }
 
 // max(x, 0.01f) of CalcAttenuation (LightingUtil.hlsl:38) as one v_med3_f32(x, 0.01, 2^100): the
@@ -239,7 +269,7 @@ __device__ __forceinline__ v2 max_dsat(v2 dist) {
 // fast path is then finite; pbr_set_pass clears the light's window flag when its strength is not
 // finite), and adding +-0 to the running sum is the identity the reference's skipped light is. Lanes
 // outside the window are redone by the caller whether lit or not.
-template <bool SPOT, bool LEAN>
+template <bool SPOT, bool LEAN, bool FAITHFUL = false>
 __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const f3x2& pos,
                                                  float4 s, float4 d, float4 p, m2& lit, m2& ok) {
     f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
@@ -250,13 +280,13 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     f3x2 h = normalize_x2(add3(q.v, l), ok);
     v2 dsat = max_dsat(dist);
-    v2 att = recip_nr(dsat * dsat).r;  // RN(1/y) already (see point_or_spot_light)
+    v2 att = FAITHFUL ? rcp_hw(dsat * dsat) : recip_nr(dsat * dsat).r;  // RN(1/y) already (see point_or_spot_light)
     if (SPOT) {
         v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
     att = vsel(lit, att, splat(0.0f));
-    return brdf_x2<LEAN>(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
+    return brdf_x2<LEAN, FAITHFUL>(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
 }
 
 }  // namespace pbr

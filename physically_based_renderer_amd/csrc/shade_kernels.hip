@@ -146,7 +146,7 @@ __device__ __forceinline__ float uniform_f(float x) {
 // increasing bit order, so the kept lights are summed in the reference's order. A dropped light is
 // one the reference's `d > 100` test (LightingUtil.hlsl:131) rejects for every pixel of the wave, i.e.
 // a +0 term: the result is bit-identical to the unculled pass.
-template <bool CULL, bool LEAN>
+template <bool CULL, bool LEAN, bool FAITHFUL = false>
 __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, m2 fast_ok,
                                               const float4* __restrict__ lights, const PassArgs& ps,
                                               const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total) {
@@ -154,7 +154,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     for (int j = 0; j < ps.n_dir; ++j) {  // directional: never culled
         const LightRec r = light_rec(lights, j);
         m2 ok = fast_ok & light_flag(r);
-        const f3x2 c = directional_x2<LEAN>(q, r.s, r.d, ok);
+        const f3x2 c = directional_x2<LEAN, FAITHFUL>(q, r.s, r.d, ok);
         redo |= ~ok;
         direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
     }
@@ -167,7 +167,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
             const LightRec r = light_rec(lights, j);
             m2 ok = fast_ok & light_flag(r);
             m2 lit;
-            const f3x2 c = point_or_spot_x2<SPOT, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
+            const f3x2 c = point_or_spot_x2<SPOT, LEAN, FAITHFUL>(q, pos, r.s, r.d, r.p, lit, ok);
             // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation)
             // when inside the window, and every lane outside it is redone.
             redo |= ~ok;
@@ -439,7 +439,18 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         const v2 nn = dot3(p.n, p.n);
         const bool lean_lane = ok_a && ok_b && nn.x <= 1.0f + 0x1p-20f && nn.y <= 1.0f + 0x1p-20f &&
                                on(q2.f0_nonzero.x) && on(q2.f0_nonzero.y);
-        if (lanes(!lean_lane) == 0)
+        // PBR_FLAG_FAITHFUL (host-validated: strengths, ambient and env texels >= 0): in a lean wave whose
+        // albedo is >= 0 and F0 in [0, 1] every light's contribution is >= 0, which bounds the error of the
+        // faithful divisions in the sum (brdf_x2<true, true>).
+        const bool faithful_lane =
+            ps.faithful && lean_lane && p.albedo.x.x >= 0.0f && p.albedo.y.x >= 0.0f && p.albedo.z.x >= 0.0f &&
+            p.albedo.x.y >= 0.0f && p.albedo.y.y >= 0.0f && p.albedo.z.y >= 0.0f && p.f0.x.x <= 1.0f &&
+            p.f0.y.x <= 1.0f && p.f0.z.x <= 1.0f && p.f0.x.y <= 1.0f && p.f0.y.y <= 1.0f && p.f0.z.y <= 1.0f &&
+            p.f0.x.x >= 0.0f && p.f0.y.x >= 0.0f && p.f0.z.x >= 0.0f && p.f0.x.y >= 0.0f && p.f0.y.y >= 0.0f &&
+            p.f0.z.y >= 0.0f;
+        if (ps.faithful && lanes(!faithful_lane) == 0)
+            d2 = lighting_fast<CULL, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+        else if (lanes(!lean_lane) == 0)
             d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
         else
             d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
