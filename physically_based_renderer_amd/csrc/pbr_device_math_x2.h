@@ -170,41 +170,12 @@ __device__ __forceinline__ v2 div_pi(v2 x) { return vfma(x, splat(kInvPiHi), x *
 //    near F0 or an exact cancellation (a multiple of ulp(F0)/2 >= 2^-45), so F is 0 or >= 2^-45 and
 //    ndf_g F stays inside the division window for any p: the p == 0 / p >= 2^-40 test is moot.
 //
-// FAITHFUL (PBR_FLAG_FAITHFUL, lean waves only): the divisions whose operands are well conditioned --
-// the NDF's a^2 / den, GeometrySchlickGGX(N.L), the specular term's / denominator, kD * albedo / PI and
-// the attenuation -- take the hardware reciprocal (v_rcp_f32, <= 1 ulp) times the numerator instead of
-// the correctly rounded Markstein step, and the NDF*G window test goes away. Everything upstream of
-// the ill-conditioned GGX denominator (L, dist, H = normalize(V + L), N.H, den) and the Fresnel term
-// whose 1 - F cancels at grazing angles stay exact. Each light's contribution is then within ~16
-// roundings of the reference's, and with every term of the sum >= 0 (host: strengths, ambient, env >= 0,
-// <= 64 lights; kernel: albedo >= 0, F0 in [0, 1] per wave) the output stays within 4.6e-6 relative:
-// inside the north-star 1e-5 (tests/test_gpu_faithful.py). Not bit-identical; the
-// default mode is.
-__device__ __forceinline__ v2 rcp_hw(v2 y) { return v2{__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)}; }
-constexpr float kInvPi = 0x1.45f306p-2f;  // RN(1/kPi)
-
-template <bool LEAN, bool FAITHFUL = false>
+template <bool LEAN>
 __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, m2& ok) {
-    static_assert(LEAN || !FAITHFUL, "FAITHFUL is a lean-wave variant");
     v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
     v2 n_dot_h_sqr = n_dot_h * n_dot_h;
     v2 den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
     den = kPi * den * den;
-    if (FAITHFUL) {
-        const v2 ndf = q.a_sqr * rcp_hw(den);
-        const v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
-        const v2 g = (n_dot_l * rcp_hw(n_dot_l * q.one_minus_k + q.k)) * q.ggx_v;
-        const v2 cos_theta = dot3_sat(h, q.v);
-        const v2 p = pow5_light(1.0f - cos_theta);
-        const f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
-        const v2 ndf_g = ndf * g;
-        const v2 rden = rcp_hw(q.four_n_dot_v * n_dot_l + 0.001f);
-        const f3x2 spec = f3x2{(ndf_g * f.x) * rden, (ndf_g * f.y) * rden, (ndf_g * f.z) * rden};
-        const f3x2 kd = f3x2{(1.0f - f.x) * q.one_minus_metal, (1.0f - f.y) * q.one_minus_metal, (1.0f - f.z) * q.one_minus_metal};
-        return f3x2{((((kd.x * q.albedo.x) * kInvPi) + spec.x) * radiance.x) * n_dot_l,
-                    ((((kd.y * q.albedo.y) * kInvPi) + spec.y) * radiance.y) * n_dot_l,
-                    ((((kd.z * q.albedo.z) * kInvPi) + spec.z) * radiance.z) * n_dot_l};
-    }
     if (!LEAN) ok &= ge(den, 0x1p-60f) & le(den, 0x1p60f);
     v2 ndf = div_nr(q.a_sqr, recip_nr(den));
     v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
@@ -245,11 +216,11 @@ __device__ __forceinline__ f3x2 normalize_x2(f3x2 v, m2& ok) {
 }
 
 // ComputeDirectionalLight, packed fast path.
-template <bool LEAN, bool FAITHFUL = false>
+template <bool LEAN>
 __device__ __forceinline__ f3x2 directional_x2(const PixelInvariants2& q, float4 s, float4 d, m2& ok) {
     f3x2 l = splat3(-d.x, -d.y, -d.z);
     f3x2 h = normalize_x2(add3(q.v, l), ok);
-    return brdf_x2<LEAN, FAITHFUL>(q, splat3(s.x, s.y, s.z), l, h, ok);
+    return brdf_x2<LEAN>(q, splat3(s.x, s.y, s.z), l, h, ok);
 }
 
 // max(x, 0.01f) of CalcAttenuation (LightingUtil.hlsl:38) as one v_med3_f32(x, 0.01, 2^100): the
@@ -269,7 +240,7 @@ __device__ __forceinline__ v2 max_dsat(v2 dist) {
 // fast path is then finite; pbr_set_pass clears the light's window flag when its strength is not
 // finite), and adding +-0 to the running sum is the identity the reference's skipped light is. Lanes
 // outside the window are redone by the caller whether lit or not.
-template <bool SPOT, bool LEAN, bool FAITHFUL = false>
+template <bool SPOT, bool LEAN>
 __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const f3x2& pos,
                                                  float4 s, float4 d, float4 p, m2& lit, m2& ok) {
     f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
@@ -280,13 +251,92 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     f3x2 h = normalize_x2(add3(q.v, l), ok);
     v2 dsat = max_dsat(dist);
-    v2 att = FAITHFUL ? rcp_hw(dsat * dsat) : recip_nr(dsat * dsat).r;  // RN(1/y) already (see point_or_spot_light)
+    v2 att = recip_nr(dsat * dsat).r;  // RN(1/y) already (see point_or_spot_light)
     if (SPOT) {
         v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
     att = vsel(lit, att, splat(0.0f));
-    return brdf_x2<LEAN, FAITHFUL>(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
+    return brdf_x2<LEAN>(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
+}
+
+// ---- PBR_FLAG_FAITHFUL: the tolerance-mode light loop (lean waves only) --------------------------------
+//
+// Exact, as in the default mode: everything upstream of the two ill-conditioned spots -- L, dist,
+// H = normalize(V + L), N.H and the GGX denominator `den` -- and the Fresnel term F, whose 1 - F cancels
+// at grazing angles. Rearranged, with the error bounded instead of bit-matched: the well-conditioned
+// rest of BRDFCookTorrance and the attenuation,
+//
+//   spec.c = NDF * G * F.c / denom = F.c * (a^2 * G1(N.V) * N.L) / (den * (N.L (1-k) + k) * denom)
+//   diff.c = (1 - F.c) * (1 - metallic) * albedo.c / PI
+//   sum.c += (diff.c + spec.c) * strength.c * (att * N.L),     att = min(RN(1/dist)^2, 1/0.01^2)
+//
+// with one hardware reciprocal (<= 1 ulp) for the three denominators, the per-pixel products
+// a^2 * G1(N.V) and (1 - metallic) * albedo / PI hoisted out of the loop, and fused multiply-adds
+// (single roundings) for the diffuse term, the diffuse + specular sum and the accumulation. Each light's
+// term stays within 32 roundings (2^-24 each) of the reference's; with every term >= 0 (host: strengths,
+// ambient, env texels >= 0, <= 64 lights; per wave: albedo >= 0, F0 in [0, 1]) the output is within
+// 4.6e-6 relative -- inside the north-star 1e-5 -- but not bit-identical.
+__device__ __forceinline__ v2 rcp_hw(v2 y) { return v2{__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)}; }
+constexpr float kInvPi = 0x1.45f306p-2f;  // RN(1/kPi)
+
+struct Faithful2 {
+    v2 a2gv;     // a^2 * GeometrySchlickGGX(N.V)
+    f3x2 mabpi;  // (1 - metallic) * albedo / PI
+};
+__device__ __forceinline__ Faithful2 make_faithful(const PixelInvariants2& q) {
+    return Faithful2{q.a_sqr * q.ggx_v, f3x2{(q.one_minus_metal * q.albedo.x) * kInvPi,
+                                            (q.one_minus_metal * q.albedo.y) * kInvPi,
+                                            (q.one_minus_metal * q.albedo.z) * kInvPi}};
+}
+
+// BRDFCookTorrance * radiance * N.L added into `sum`; `att` = the light's attenuation (1 for
+// directional lights), already 0 for lanes beyond the range.
+__device__ __forceinline__ void brdf_faithful_x2(const PixelInvariants2& q, const Faithful2& fi, float4 s, v2 att,
+                                                 f3x2 l, f3x2 h, f3x2& sum) {
+    const v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
+    v2 den = ((n_dot_h * n_dot_h) * q.a_sqr_minus_1 + 1.0f);  // exact: the ill-conditioned GGX denominator
+    den = kPi * den * den;
+    const v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
+    const v2 r = rcp_hw((den * (n_dot_l * q.one_minus_k + q.k)) * (q.four_n_dot_v * n_dot_l + 0.001f));
+    const v2 p = pow5_light(1.0f - dot3_sat(h, q.v));
+    const f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
+    const v2 kr = (fi.a2gv * n_dot_l) * r;
+    const v2 w = att * n_dot_l;
+    sum.x = vfma(vfma(kr, f.x, vfma(-f.x, fi.mabpi.x, fi.mabpi.x)), s.x * w, sum.x);
+    sum.y = vfma(vfma(kr, f.y, vfma(-f.y, fi.mabpi.y, fi.mabpi.y)), s.y * w, sum.y);
+    sum.z = vfma(vfma(kr, f.z, vfma(-f.z, fi.mabpi.z, fi.mabpi.z)), s.z * w, sum.z);
+}
+
+__device__ __forceinline__ void directional_faithful_x2(const PixelInvariants2& q, const Faithful2& fi, float4 s,
+                                                        float4 d, m2& ok, f3x2& sum) {
+    const f3x2 l = splat3(-d.x, -d.y, -d.z);
+    const f3x2 h = normalize_x2(add3(q.v, l), ok);
+    brdf_faithful_x2(q, fi, s, splat(1.0f), l, h, sum);
+}
+
+template <bool SPOT>
+__device__ __forceinline__ void point_or_spot_faithful_x2(const PixelInvariants2& q, const Faithful2& fi,
+                                                          const f3x2& pos, float4 s, float4 d, float4 p, m2& ok,
+                                                          f3x2& sum) {
+    f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
+    const v2 dist = sqrt_nr(dot3(l, l));
+    const m2 lit = not_gt(dist, kLightRange);
+    ok &= ge(dist, 0x1p-20f);
+    const Recip2 rdist = recip_nr(dist);
+    l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
+    const f3x2 h = normalize_x2(add3(q.v, l), ok);
+    // 1 / max(dist, 0.01)^2 (LightingUtil.hlsl:35-40) from the correctly rounded RN(1/dist) the exact L
+    // already needs: dist >= 0.01 <=> RN(1/dist) <= 100, so the clamp is a min against the constant.
+    constexpr float kAttMax = 1.0f / (0.01f * 0.01f);
+    v2 att = rdist.r * rdist.r;
+    att = v2{fminf(att.x, kAttMax), fminf(att.y, kAttMax)};
+    if (SPOT) {
+        const v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
+        att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
+    }
+    att = vsel(lit, att, splat(0.0f));  // beyond the range: +0 (see point_or_spot_x2)
+    brdf_faithful_x2(q, fi, s, att, l, h, sum);
 }
 
 }  // namespace pbr

@@ -150,13 +150,20 @@ template <bool CULL, bool LEAN, bool FAITHFUL = false>
 __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, m2 fast_ok,
                                               const float4* __restrict__ lights, const PassArgs& ps,
                                               const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total) {
+    static_assert(LEAN || !FAITHFUL, "the faithful loop is a lean-wave variant");
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
+    Faithful2 fi{};
+    if (FAITHFUL) fi = make_faithful(q);
     for (int j = 0; j < ps.n_dir; ++j) {  // directional: never culled
         const LightRec r = light_rec(lights, j);
         m2 ok = fast_ok & light_flag(r);
-        const f3x2 c = directional_x2<LEAN, FAITHFUL>(q, r.s, r.d, ok);
+        if (FAITHFUL) {
+            directional_faithful_x2(q, fi, r.s, r.d, ok, direct);
+        } else {
+            const f3x2 c = directional_x2<LEAN>(q, r.s, r.d, ok);
+            direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
+        }
         redo |= ~ok;
-        direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
     }
     const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
     // Point lights, then spot lights: one loop each (SPOT is a template constant, so the point loop
@@ -166,12 +173,16 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         auto point = [&](int j) {
             const LightRec r = light_rec(lights, j);
             m2 ok = fast_ok & light_flag(r);
-            m2 lit;
-            const f3x2 c = point_or_spot_x2<SPOT, LEAN, FAITHFUL>(q, pos, r.s, r.d, r.p, lit, ok);
             // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation)
             // when inside the window, and every lane outside it is redone.
+            if (FAITHFUL) {
+                point_or_spot_faithful_x2<SPOT>(q, fi, pos, r.s, r.d, r.p, ok, direct);
+            } else {
+                m2 lit;
+                const f3x2 c = point_or_spot_x2<SPOT, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
+                direct = add3(direct, c);
+            }
             redo |= ~ok;
-            direct = add3(direct, c);
         };
         if (!CULL) {
             for (int j = b0; j < b1; ++j) point(j);
@@ -198,6 +209,17 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     };
     run_kind(std::false_type{}, pt_begin, sp_begin);
     if (end > sp_begin) run_kind(std::true_type{}, sp_begin, end);
+    if (FAITHFUL) {
+        // The faithful loop's relative bound holds for sums of normal-range values: a nonzero sum
+        // outside [2^-100, 2^100] (tiny sums, where underflowed terms -- a spot cone's pow, say -- carry
+        // absolute errors of ~2^-149 that are not small relative to the sum; NaN; overflow) is redone
+        // exactly. A zero sum (no light reaches the pixel: every N.L or attenuation is 0, exactly as in
+        // the reference) is kept; DESIGN.md §2 states the one residue.
+        const m2 in_x = eq(direct.x, 0.0f) | (ge(direct.x, 0x1p-100f) & le(direct.x, 0x1p100f));
+        const m2 in_y = eq(direct.y, 0.0f) | (ge(direct.y, 0x1p-100f) & le(direct.y, 0x1p100f));
+        const m2 in_z = eq(direct.z, 0.0f) | (ge(direct.z, 0x1p-100f) & le(direct.z, 0x1p100f));
+        redo |= ~(in_x & in_y & in_z);
+    }
     return direct;
 }
 
