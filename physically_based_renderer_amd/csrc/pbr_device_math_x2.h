@@ -297,7 +297,10 @@ __device__ __forceinline__ void brdf_faithful_x2(const PixelInvariants2& q, cons
     const v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
     v2 den = ((n_dot_h * n_dot_h) * q.a_sqr_minus_1 + 1.0f);  // exact: the ill-conditioned GGX denominator
     den = kPi * den * den;
-    const v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
+    // saturate instead of max(., 0): N.L is not on the ill-conditioned chain, and in lean waves it
+    // exceeds 1 by at most 2^-20.6 (|N|^2 <= 1 + 2^-20, |L| <= 1 + 2^-23), a relative change the bound
+    // absorbs; the clamp rides on the dot's last add.
+    const v2 n_dot_l = dot3_sat(q.n, l);
     const v2 r = rcp_hw((den * (n_dot_l * q.one_minus_k + q.k)) * (q.four_n_dot_v * n_dot_l + 0.001f));
     const v2 p = pow5_light(1.0f - dot3_sat(h, q.v));
     const f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};

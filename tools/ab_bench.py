@@ -17,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def one(lib: str, cid: int, reps: int) -> dict:
+def one(lib: str, cid: int, reps: int, flags: int = 0) -> dict:
     os.environ["PBR_LIB_PATH"] = os.path.abspath(lib)
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -31,6 +31,7 @@ def one(lib: str, cid: int, reps: int) -> dict:
     cfg = S.CONFIGS[cid]
     planes, _ = S.fill_gbuffer_host(cfg)
     pc = S.scene_pass(cfg)
+    pc.flags = int(pc.flags) | flags
     dev = torch.device("cuda", 0)
     gb = GBuffer.from_host(planes, dev)
     out = torch.empty((cfg.height, cfg.width, 4), device=dev)
@@ -59,17 +60,19 @@ def main():
     ap.add_argument("--configs", nargs="+", type=int, default=[3])
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--flags", type=int, default=0, help="extra pass flags, e.g. 16 = PBR_FLAG_FAITHFUL")
     ap.add_argument("--one", nargs=2, help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.one:
-        print(json.dumps(one(a.one[0], int(a.one[1]), a.reps)), flush=True)
+        print(json.dumps(one(a.one[0], int(a.one[1]), a.reps, a.flags)), flush=True)
         return
     results = {}
     for r in range(a.rounds):
         order = a.libs if r % 2 == 0 else list(reversed(a.libs))
         for cid in a.configs:
             for lib in order:
-                p = subprocess.run([sys.executable, __file__, "--libs", lib, "--reps", str(a.reps), "--one", lib, str(cid)],
+                p = subprocess.run([sys.executable, __file__, "--libs", lib, "--reps", str(a.reps), "--flags", str(a.flags),
+                                    "--one", lib, str(cid)],
                                    capture_output=True, text=True, timeout=300)
                 if p.returncode != 0:
                     print(p.stdout, p.stderr, file=sys.stderr)
