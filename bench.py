@@ -90,10 +90,17 @@ def load_pmc(workload: str):
         return None, None
 
 
-def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int):
-    """Time the CPU oracle on every k-th row of the frame (rank 0, N = 1) and check parity there."""
+def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int, kind: str = "auto"):
+    """Time the reference CPU shader path on every k-th row of the frame (rank 0, N = 1) and check parity
+    there. kind "reference": the reference's own LightingUtil.hlsl compiled as C++ (oracle/_ref, built in
+    the build container; nothing under /root/reference is read at run time), one row band per host thread;
+    kind "port": the C restatement oracle/pbr_oracle.c (pthreads). "auto" takes the reference build when
+    it is present. Both are test infrastructure, used here only as the CPU baseline and the checker."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import oracle as O  # test infrastructure: the checker / CPU baseline only
 
+    use_ref = kind == "reference" or (kind == "auto" and O.ref_available())
     n_threads = max(1, min(16, len(os.sched_getaffinity(0))))
     step = max(1, cfg.height // budget_rows) if budget_rows > 0 else 1
     sample = np.ascontiguousarray(planes_host[:, ::step])
@@ -102,14 +109,24 @@ def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int):
                        n_spot=pc.num_spot_lights, ambient_mode=pc.ambient_mode,
                        use_f0_plane=bool(pc.flags & N.PBR_FLAG_F0_PLANE),
                        apply_ao=bool(pc.flags & N.PBR_FLAG_APPLY_AO))
+    lights = pc.light_array()
+
+    def run(planes, threads):
+        if not use_ref:
+            return O.shade(list(planes), ops, lights, env, n_threads=threads)
+        edges = np.linspace(0, planes.shape[1], threads + 1).astype(int)
+        bands = [np.ascontiguousarray(planes[:, a:b]) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+        with ThreadPoolExecutor(len(bands)) as ex:  # ctypes releases the GIL inside each call
+            return np.concatenate(list(ex.map(lambda b: O.shade_ref(list(b), ops, lights, env), bands)), axis=0)
+
     t0 = time.perf_counter()
-    ref = O.shade(list(sample), ops, pc.light_array(), env, n_threads=n_threads)
+    ref = run(sample, n_threads)
     dt = time.perf_counter() - t0
     px = sample.shape[1] * sample.shape[2]
     # single-thread rate on the first 8 sampled rows (single-thread and all-core)
     one = np.ascontiguousarray(sample[:, :8])
     t1 = time.perf_counter()
-    O.shade(list(one), ops, pc.light_array(), env, n_threads=1)
+    run(one, 1)
     st = one.shape[1] * one.shape[2] / (time.perf_counter() - t1) / 1e6
     got = gpu_frame[::step]
     err = O.rel_err(got, ref)
@@ -122,13 +139,16 @@ def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int):
                 break
     except OSError:
         pass
+    what = ("oracle/_ref/libpbr_ref.so: the reference's LightingUtil.hlsl compiled as C++ (g++ -O2 "
+            f"-ffp-contract=off), {n_threads} host threads over row bands" if use_ref else
+            f"oracle/pbr_oracle.c, -O2 -ffp-contract=off, {n_threads} pthreads")
     return {
-        "value": round(px / dt / 1e6, 4), "unit": "Mpix/s", "cores": n_threads, "kind": "port",
+        "value": round(px / dt / 1e6, 4), "unit": "Mpix/s", "cores": n_threads,
+        "kind": "reference" if use_ref else "port",
         "cpu_model": model,
         "single_thread_value": round(st, 4),
         "sample": (f"every {step}th row of" if step > 1 else "all rows of") +
-                  f" the same {cfg.width}x{cfg.height} frame ({px} px, {dt:.2f} s wall), "
-                  f"oracle/pbr_oracle.c, -O2 -ffp-contract=off, {n_threads} pthreads",
+                  f" the same {cfg.width}x{cfg.height} frame ({px} px, {dt:.2f} s wall), {what}",
     }, float(err.max()), exact, (step, ref)
 
 
@@ -193,6 +213,9 @@ def main():
     ap.add_argument("--exact-leg", action="store_true",
                     help="N = 1, faithful mode: also time the exact mode on the same G-buffer and report it as exact_mode "
                          "(off by default so that a kernel trace of the default command holds only the headline launches)")
+    ap.add_argument("--cpu-kind", default="auto", choices=["auto", "reference", "port"],
+                    help="CPU baseline: the reference's own shader source compiled for the host (oracle/_ref) or the "
+                         "C restatement (oracle/pbr_oracle.c); auto = the reference build when present")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="rows in the CPU-baseline sample (0 = the whole frame: ~1.5 s on 16 host threads)")
     args = ap.parse_args()
@@ -377,7 +400,7 @@ def main():
         if world == 1 and args.mode == "faithful" and args.exact_leg:
             exact_leg = time_exact_mode(ctx, pc, gb, outs[0], stream, args, fmt, rgba8, cfg.width * band.rows)
         if frame is not None and not args.no_cpu_baseline:
-            cpu, max_rel, exact, (step, ref) = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows)
+            cpu, max_rel, exact, (step, ref) = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows, args.cpu_kind)
             parity = {"parity_max_rel": max_rel, "parity_bit_exact_frac": round(exact, 6)}
             if exact_leg is not None:
                 from oracle import oracle as O  # test infrastructure: the checker only

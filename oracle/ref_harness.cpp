@@ -1,5 +1,7 @@
 // oracle/ref_harness.cpp -- TEST INFRASTRUCTURE ONLY.  Built into oracle/_ref/libpbr_ref.so by
-// oracle/Makefile, and only where /root/reference exists (this container; never the GPU box).
+// oracle/Makefile, and only where /root/reference exists (the build container). The built library reads
+// nothing from /root/reference at run time; it travels with the tree and serves bench.py's CPU baseline
+// (kind "reference"). Stateless: every entry point may run concurrently on disjoint row bands.
 //
 // The reference's own light/BRDF code -- /root/reference/Source/Shaders/LightingUtil.hlsl, included
 // UNMODIFIED by absolute path -- compiled as C++ on top of hlsl_prelude.hpp. It is included once
