@@ -145,6 +145,16 @@ __device__ __forceinline__ float pow_inv_gamma(float c) {
         return pbr_powf_exp2((double)kInvGamma * pbr_powf_log2(ix, PBR_LIBM_LOG2_TAB), 0u, PBR_LIBM_EXP2_TAB);
     return pbr_powf(c, kInvGamma);
 }
+// PBR_FLAG_FAITHFUL's gamma encode: exp2(kInvGamma * log2(c)) on the hardware v_log_f32 / v_exp_f32
+// for c in [kFaithfulGammaLo, 1) -- every tonemapped value c/(c+1) of a lit channel but the darkest --
+// and glibc's powf elsewhere. Error vs glibc powf measured exhaustively on the GPU
+// (tests/hip/gamma_probe.hip): DESIGN.md §2 adds it to the faithful bound.
+constexpr float kFaithfulGammaLo = 0x1p-10f;
+__device__ __forceinline__ float pow_inv_gamma_faithful(float c) {
+    if (__builtin_expect(c >= kFaithfulGammaLo && c < 1.0f, 1))
+        return __builtin_amdgcn_exp2f(kInvGamma * __builtin_amdgcn_logf(c));
+    return pow_inv_gamma(c);
+}
 constexpr float kLightRange = 100.0f;     // LightingUtil.hlsl:131
 
 // Everything BRDFCookTorrance (LightingUtil.hlsl:85-104) needs that does not depend on the light.

@@ -319,10 +319,13 @@ __device__ __forceinline__ float reinhard(float c, bool fast) {
     if (fast && (c == 0.0f || (c >= 0x1p-100f && c <= 0x1p60f))) return div_nr(c, recip_nr(c + 1.0f));
     return c / (c + 1.0f);
 }
+// PBR_FLAG_FAITHFUL waves: Reinhard with the hardware reciprocal (c >= 0 here; inf / NaN give NaN as
+// the IEEE quotient does) and the gamma encode of pow_inv_gamma_faithful.
+__device__ __forceinline__ float reinhard_faithful(float c) { return c * __builtin_amdgcn_rcpf(c + 1.0f); }
 
 template <int AMBIENT, bool APPLY_AO>
 __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float ao, f3 direct, const PassArgs& ps,
-                                               const float4* __restrict__ env, bool fast) {
+                                               const float4* __restrict__ env, bool fast, bool faithful = false) {
     const PixelInvariants& q = p;
     f3 ambient;
     if (AMBIENT == kAmbientIblDiffuse) {
@@ -344,6 +347,11 @@ __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float a
     }
     if (APPLY_AO) ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
     f3 lit = add3(ambient, direct);
+    if (faithful) {  // wave-uniform
+        lit = mk3(reinhard_faithful(lit.x), reinhard_faithful(lit.y), reinhard_faithful(lit.z));
+        return make_float4(pow_inv_gamma_faithful(lit.x), pow_inv_gamma_faithful(lit.y),
+                           pow_inv_gamma_faithful(lit.z), ps.opacity);
+    }
     lit = mk3(reinhard(lit.x, fast), reinhard(lit.y, fast), reinhard(lit.z, fast));  // Default.hlsl:153
     return make_float4(pow_inv_gamma(lit.x), pow_inv_gamma(lit.y), pow_inv_gamma(lit.z),
                        ps.opacity);
@@ -456,6 +464,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const f3x2 pos2 = p.pos;
     const float ao_a = p.ao.x, ao_b = p.ao.y;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
+    bool faithful_wave = false;  // wave-uniform: the faithful loop ran, so the finish may be faithful too
     if (wave_geometry) {  // wave-uniform
         // Wave-uniform choice of the light loop.
         const v2 nn = dot3(p.n, p.n);
@@ -470,7 +479,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             p.f0.y.x <= 1.0f && p.f0.z.x <= 1.0f && p.f0.x.y <= 1.0f && p.f0.y.y <= 1.0f && p.f0.z.y <= 1.0f &&
             p.f0.x.x >= 0.0f && p.f0.y.x >= 0.0f && p.f0.z.x >= 0.0f && p.f0.x.y >= 0.0f && p.f0.y.y >= 0.0f &&
             p.f0.z.y >= 0.0f;
-        if (ps.faithful && lanes(!faithful_lane) == 0)
+        faithful_wave = ps.faithful && lanes(!faithful_lane) == 0;
+        if (faithful_wave)
             d2 = lighting_fast<CULL, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
         else if (lanes(!lean_lane) == 0)
             d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
@@ -504,10 +514,10 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 
     const int64_t orow = (int64_t)y * fr.out_stride;
     if (va)
-        store_pixel(fr, orow + xa, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a)
+        store_pixel(fr, orow + xa, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
                                       : sky_pixel(ua.n, ps, fr.sky, !exact_only));
     if (vb)
-        store_pixel(fr, orow + xa + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b)
+        store_pixel(fr, orow + xa + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
                                            : sky_pixel(ub.n, ps, fr.sky, !exact_only));
 }
 

@@ -26,7 +26,7 @@ FLAGS = ["-O3", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result", "-fPIC"
 def probes(tmp_path_factory, gpu):
     d = tmp_path_factory.mktemp("probes")
     libs = {}
-    for name in ("fastdiv_probe", "libm_probe", "sqrt_probe"):
+    for name in ("fastdiv_probe", "libm_probe", "sqrt_probe", "gamma_probe"):
         so = str(d / f"{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, os.path.join(ROOT, "tests", "hip", f"{name}.hip"), "-o", so,
                         "-lpthread"], check=True)
@@ -89,3 +89,19 @@ def test_device_atan2f_pairs_equal_glibc(probes):
     y, x = ctypes.c_float(), ctypes.c_float()
     bad = L.probe_atan2_pairs(2024, 1 << 27, ctypes.byref(y), ctypes.byref(x))
     assert bad == 0, f"{bad} mismatches, first atan2f({y.value!r}, {x.value!r})"
+
+
+def test_faithful_gamma_error_exhaustive(probes):
+    """PBR_FLAG_FAITHFUL's gamma encode vs the host glibc powf(c, 1/2.2f) on every float of the binades
+    [2^-14, 1): within 5.4e-7 relative (9 x 2^-24) where the hardware exp2/log2 path runs (c >= 2^-10),
+    bit-identical below it (the glibc algorithm). DESIGN.md §2 adds this to the faithful bound."""
+    L = probes["gamma_probe"]
+    lo, hi = -14, -1
+    out = (ctypes.c_double * (hi - lo + 1))()
+    assert L.probe_gamma(lo, hi, out) == 0
+    for e in range(lo, hi + 1):
+        print(f"binade 2^{e}: max_rel {out[e - lo]:.3g}")
+        if e >= -10:
+            assert out[e - lo] <= 5.4e-7, e
+        else:
+            assert out[e - lo] == 0.0, e

@@ -1,7 +1,7 @@
 """Kernel time vs light count on a fixed G-buffer: separates the per-pixel fixed cost (V, BRDF
 invariants, ambient, tonemap, gamma) from the per-light cost. Prints one line per light count.
 
-    python tools/light_sweep.py [--width 3840 --height 2160] [--ibl]
+    python tools/light_sweep.py [--width 3840 --height 2160] [--ibl] [--flags 16]
 """
 import argparse
 import os
@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--ibl", action="store_true")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--flags", type=int, default=0, help="extra pass flags, e.g. 16 = PBR_FLAG_FAITHFUL")
     a = ap.parse_args()
     cfg = S.CONFIGS[3].with_size(a.width, a.height)
     planes, _ = S.fill_gbuffer_host(cfg)
@@ -40,7 +41,8 @@ def main():
         prev = None
         for n in (0, 1, 2, 4, 8, 16, 32, 64):
             pc = PassConstants(eye_pos_w=base.eye_pos_w, num_point_lights=n, lights_array=lights[:max(n, 1)],
-                               ambient_mode=N.PBR_AMBIENT_IBL_DIFFUSE if a.ibl else N.PBR_AMBIENT_CONSTANT)
+                               ambient_mode=N.PBR_AMBIENT_IBL_DIFFUSE if a.ibl else N.PBR_AMBIENT_CONSTANT,
+                               flags=a.flags)
             ctx.set_pass(pc)
             for _ in range(3):
                 ctx.shade(gb, out)
