@@ -70,7 +70,7 @@ enum pbr_pass_flags {
                                          attenuation) use the hardware reciprocal (<= 1 ulp) instead of
                                          correct rounding; the ill-conditioned GGX chain and Fresnel stay
                                          exact. Output within 1e-5 relative of the reference evaluation
-                                         (the north-star bar; bound 5.4e-6, measured 6.1e-7), not bit-identical.
+                                         (the north-star bar; bound 5.9e-6, measured 6.3e-7), not bit-identical.
                                          Applies where every light term is >= 0 and the sum is short:
                                          <= 64 lights, non-negative strengths, ambient and env texels
                                          (checked on the host), albedo >= 0 and F0 in [0, 1] (checked per

@@ -276,7 +276,7 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
 // (single roundings) for the diffuse term, the diffuse + specular sum and the accumulation. Each light's
 // term stays within 38 roundings (2^-24 each) of the reference's; with every term >= 0 (host: strengths,
 // ambient, env texels >= 0, <= 64 lights; per wave: albedo >= 0, F0 in [0, 1]) the output is within
-// 5.4e-6 relative with the faithful finish -- inside the north-star 1e-5 -- but not bit-identical.
+// 5.9e-6 relative with the faithful finish -- inside the north-star 1e-5 -- but not bit-identical.
 __device__ __forceinline__ v2 rcp_hw(v2 y) { return v2{__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)}; }
 constexpr float kInvPi = 0x1.45f306p-2f;  // RN(1/kPi)
 
