@@ -72,7 +72,8 @@ enum pbr_pass_flags {
                                          exact. Output within 1e-5 relative of the reference evaluation
                                          (the north-star bar; bound 5.9e-6, measured 6.3e-7), not bit-identical.
                                          Applies where every light term is >= 0 and the sum is short:
-                                         <= 64 lights, non-negative strengths, ambient and env texels
+                                         <= 64 lights (with PBR_FLAG_TILED_CULLING: <= 64 surviving lights,
+                                         counted per wave), non-negative strengths, ambient and env texels
                                          (checked on the host), albedo >= 0 and F0 in [0, 1] (checked per
                                          wave); elsewhere the pass stays exact. */
 };

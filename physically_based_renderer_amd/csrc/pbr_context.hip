@@ -40,6 +40,7 @@ struct pbr_context {
     uint32_t flags = 0;
     bool pass_set = false;
     bool faithful_pass_ok = false;  // light strengths and the constant ambient are finite and >= 0
+    bool faithful_count_terms = false;  // > 64 lights (culled pass): the kernel counts summed terms per wave
     // Statistics of the last pass: one record of pbr::kStatsPerBlock int32 per workgroup ([surviving
     // point/spot lights summed over its culling tiles, culling tiles with geometry, pixels redone by the
     // exact path]), summed on the host by pbr_last_pass_stats / pbr_last_cull_stats.
@@ -227,9 +228,11 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
     p.n_point = np;
     p.n_spot = ns;
     // PBR_FLAG_FAITHFUL's error bound needs every term of the light sum >= 0
-    // (pbr_device_math_x2.h, brdf_x2<true, true>): finite non-negative strengths and a non-negative
-    // constant ambient; and at most 64 lights, since the sum's rounding drift grows by <= 1 ulp per term.
-    bool nonneg = n <= 64;
+    // (pbr_device_math_x2.h, brdf_faithful_x2): finite non-negative strengths and a non-negative constant
+    // ambient; and at most 64 summed terms, since the sum's rounding drift grows by <= 1 ulp per term --
+    // with tiled culling the kernel counts each wave's surviving lights (faithful mode 2).
+    ctx->faithful_count_terms = n > 64;
+    bool nonneg = n <= 64 || (pass->flags & PBR_FLAG_TILED_CULLING) != 0;
     for (long long i = 0; i < n; ++i)
         for (int k = 0; k < 3; ++k) nonneg = nonneg && std::isfinite(pass->lights[i].strength[k]) && pass->lights[i].strength[k] >= 0.0f;
     if (pass->ambient_mode == PBR_AMBIENT_CONSTANT)
@@ -346,6 +349,7 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     a.exact_only = (ctx->flags & PBR_FLAG_EXACT_ONLY) != 0;
     a.ps.faithful = (ctx->flags & PBR_FLAG_FAITHFUL) && !a.exact_only && ctx->faithful_pass_ok &&
                     (ctx->ambient_mode != PBR_AMBIENT_IBL_DIFFUSE || ctx->env.nonneg);
+    if (a.ps.faithful && ctx->faithful_count_terms) a.ps.faithful = 2;
     a.pixels_per_thread = ctx->pixels_per_thread;
 
     DeviceGuard g(ctx->device);

@@ -291,16 +291,20 @@ __device__ __forceinline__ Faithful2 make_faithful(const PixelInvariants2& q) {
 }
 
 // BRDFCookTorrance * radiance * N.L added into `sum`; `att` = the light's attenuation (1 for
-// directional lights), already 0 for lanes beyond the range.
+// directional lights), already 0 for lanes beyond the range. LEAN as in brdf_x2: outside lean waves
+// (|N| up to the window's bound, zero F0 components) `den` is tested against [2^-60, 2^60] so that the
+// product of the three denominators stays normal, and N.L keeps its max(., 0).
+template <bool LEAN>
 __device__ __forceinline__ void brdf_faithful_x2(const PixelInvariants2& q, const Faithful2& fi, float4 s, v2 att,
-                                                 f3x2 l, f3x2 h, f3x2& sum) {
+                                                 f3x2 l, f3x2 h, m2& ok, f3x2& sum) {
     const v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
     v2 den = ((n_dot_h * n_dot_h) * q.a_sqr_minus_1 + 1.0f);  // exact: the ill-conditioned GGX denominator
     den = kPi * den * den;
-    // saturate instead of max(., 0): N.L is not on the ill-conditioned chain, and in lean waves it
+    if (!LEAN) ok &= ge(den, 0x1p-60f) & le(den, 0x1p60f);
+    // Lean waves: saturate instead of max(., 0). N.L is not on the ill-conditioned chain, and there it
     // exceeds 1 by at most 2^-20.6 (|N|^2 <= 1 + 2^-20, |L| <= 1 + 2^-23), a relative change the bound
     // absorbs; the clamp rides on the dot's last add.
-    const v2 n_dot_l = dot3_sat(q.n, l);
+    const v2 n_dot_l = LEAN ? dot3_sat(q.n, l) : vmax(dot3(q.n, l), splat(0.0f));
     const v2 r = rcp_hw((den * (n_dot_l * q.one_minus_k + q.k)) * (q.four_n_dot_v * n_dot_l + 0.001f));
     const v2 p = pow5_light(1.0f - dot3_sat(h, q.v));
     const f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
@@ -311,14 +315,15 @@ __device__ __forceinline__ void brdf_faithful_x2(const PixelInvariants2& q, cons
     sum.z = vfma(vfma(kr, f.z, vfma(-f.z, fi.mabpi.z, fi.mabpi.z)), s.z * w, sum.z);
 }
 
+template <bool LEAN>
 __device__ __forceinline__ void directional_faithful_x2(const PixelInvariants2& q, const Faithful2& fi, float4 s,
                                                         float4 d, m2& ok, f3x2& sum) {
     const f3x2 l = splat3(-d.x, -d.y, -d.z);
     const f3x2 h = normalize_x2(add3(q.v, l), ok);
-    brdf_faithful_x2(q, fi, s, splat(1.0f), l, h, sum);
+    brdf_faithful_x2<LEAN>(q, fi, s, splat(1.0f), l, h, ok, sum);
 }
 
-template <bool SPOT>
+template <bool SPOT, bool LEAN>
 __device__ __forceinline__ void point_or_spot_faithful_x2(const PixelInvariants2& q, const Faithful2& fi,
                                                           const f3x2& pos, float4 s, float4 d, float4 p, m2& ok,
                                                           f3x2& sum) {
@@ -339,7 +344,7 @@ __device__ __forceinline__ void point_or_spot_faithful_x2(const PixelInvariants2
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
     att = vsel(lit, att, splat(0.0f));  // beyond the range: +0 (see point_or_spot_x2)
-    brdf_faithful_x2(q, fi, s, att, l, h, sum);
+    brdf_faithful_x2<LEAN>(q, fi, s, att, l, h, ok, sum);
 }
 
 }  // namespace pbr

@@ -42,6 +42,8 @@ constexpr int kChunk = 256;  // lights staged per LDS pass
 // Conservative cull radius: d_fp32 >= d_true * (1 - 4.8e-7) (three roundings in L, three in the
 // dot, one in sqrt); a margin of 1e-4 relative covers that and the fp32 box-distance error.
 constexpr float kCullRadius = 100.01f;
+// PBR_FLAG_FAITHFUL: the most light terms a pixel's sum may have for the mode's error bound.
+constexpr int kFaithfulMaxTerms = 64;
 
 struct TileBounds {
     float mn[3], mx[3];
@@ -138,6 +140,30 @@ __device__ __forceinline__ float uniform_f(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
 }
 
+// The tiled-culling range test: point/spot light `lp` may be within range of some point of the box `wb`
+// (the box distance against the conservative radius kCullRadius).
+__device__ __forceinline__ bool light_survives(float4 lp, const TileBounds& wb) {
+    const float dx = hmax(hmax(wb.mn[0] - lp.x, lp.x - wb.mx[0]), 0.0f);
+    const float dy = hmax(hmax(wb.mn[1] - lp.y, lp.y - wb.mx[1]), 0.0f);
+    const float dz = hmax(hmax(wb.mn[2] - lp.z, lp.z - wb.mx[2]), 0.0f);
+    return (dx * dx + dy * dy + dz * dz) <= kCullRadius * kCullRadius;
+}
+
+// The number of light terms the wave sums under tiled culling: directional lights + the point/spot lights
+// that survive its box (one lane per light, the same test as the loop). PBR_FLAG_FAITHFUL's bound counts
+// summed terms, so a culled pass with more lights than the bound allows can still run it per wave.
+__device__ __forceinline__ int wave_light_terms(const float4* __restrict__ lights, const PassArgs& ps,
+                                                const TileBounds& wb, bool cull_enabled) {
+    const int b0 = ps.n_dir, b1 = ps.n_dir + ps.n_point + ps.n_spot;
+    if (!cull_enabled) return b1;
+    int total = ps.n_dir;
+    for (int base = b0; base < b1; base += 64) {
+        const int j = base + (int)(threadIdx.x & 63);
+        total += __popcll(lanes(j < b1 && light_survives(lights[3 * j + 2], wb)));
+    }
+    return total;
+}
+
 // ComputeLighting (LightingUtil.hlsl:170-200) for both pixels of the pair on the packed fast path:
 // in-order sum from +0; `redo` collects pixels that left the fast-path window for a lit light.
 // LEAN (wave-uniform): the wave's pixels satisfy the extra conditions of brdf_x2<true>.
@@ -150,7 +176,6 @@ template <bool CULL, bool LEAN, bool FAITHFUL = false>
 __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, m2 fast_ok,
                                               const float4* __restrict__ lights, const PassArgs& ps,
                                               const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total) {
-    static_assert(LEAN || !FAITHFUL, "the faithful loop is a lean-wave variant");
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     Faithful2 fi{};
     if (FAITHFUL) fi = make_faithful(q);
@@ -158,7 +183,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         const LightRec r = light_rec(lights, j);
         m2 ok = fast_ok & light_flag(r);
         if (FAITHFUL) {
-            directional_faithful_x2(q, fi, r.s, r.d, ok, direct);
+            directional_faithful_x2<LEAN>(q, fi, r.s, r.d, ok, direct);
         } else {
             const f3x2 c = directional_x2<LEAN>(q, r.s, r.d, ok);
             direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
@@ -176,7 +201,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
             // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation)
             // when inside the window, and every lane outside it is redone.
             if (FAITHFUL) {
-                point_or_spot_faithful_x2<SPOT>(q, fi, pos, r.s, r.d, r.p, ok, direct);
+                point_or_spot_faithful_x2<SPOT, LEAN>(q, fi, pos, r.s, r.d, r.p, ok, direct);
             } else {
                 m2 lit;
                 const f3x2 c = point_or_spot_x2<SPOT, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
@@ -191,13 +216,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         for (int base = b0; base < b1; base += 64) {
             const int j = base + (int)(threadIdx.x & 63);
             bool keep = j < b1;
-            if (keep && cull_enabled) {
-                const float4 lp = lights[3 * j + 2];
-                const float dx = hmax(hmax(wb.mn[0] - lp.x, lp.x - wb.mx[0]), 0.0f);
-                const float dy = hmax(hmax(wb.mn[1] - lp.y, lp.y - wb.mx[1]), 0.0f);
-                const float dz = hmax(hmax(wb.mn[2] - lp.z, lp.z - wb.mx[2]), 0.0f);
-                keep = (dx * dx + dy * dy + dz * dz) <= kCullRadius * kCullRadius;
-            }
+            if (keep && cull_enabled) keep = light_survives(lights[3 * j + 2], wb);
             uint64_t m = lanes(keep);
             kept_total += __popcll(m);
             while (m) {
@@ -470,19 +489,25 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         const v2 nn = dot3(p.n, p.n);
         const bool lean_lane = ok_a && ok_b && nn.x <= 1.0f + 0x1p-20f && nn.y <= 1.0f + 0x1p-20f &&
                                on(q2.f0_nonzero.x) && on(q2.f0_nonzero.y);
-        // PBR_FLAG_FAITHFUL (host-validated: strengths, ambient and env texels >= 0): in a lean wave whose
-        // albedo is >= 0 and F0 in [0, 1] every light's contribution is >= 0, which bounds the error of the
-        // faithful divisions in the sum (brdf_x2<true, true>).
+        // PBR_FLAG_FAITHFUL (host-validated: strengths, ambient and env texels >= 0): in a wave inside the
+        // fast window whose albedo is >= 0 and F0 in [0, 1] every light's contribution is >= 0, which bounds
+        // the error of the faithful divisions in the sum (brdf_faithful_x2). ps.faithful == 2: a culled pass
+        // with more lights than the bound's 64 summed terms, counted per wave here.
         const bool faithful_lane =
-            ps.faithful && lean_lane && p.albedo.x.x >= 0.0f && p.albedo.y.x >= 0.0f && p.albedo.z.x >= 0.0f &&
+            ps.faithful && ok_a && ok_b && p.albedo.x.x >= 0.0f && p.albedo.y.x >= 0.0f && p.albedo.z.x >= 0.0f &&
             p.albedo.x.y >= 0.0f && p.albedo.y.y >= 0.0f && p.albedo.z.y >= 0.0f && p.f0.x.x <= 1.0f &&
             p.f0.y.x <= 1.0f && p.f0.z.x <= 1.0f && p.f0.x.y <= 1.0f && p.f0.y.y <= 1.0f && p.f0.z.y <= 1.0f &&
             p.f0.x.x >= 0.0f && p.f0.y.x >= 0.0f && p.f0.z.x >= 0.0f && p.f0.x.y >= 0.0f && p.f0.y.y >= 0.0f &&
             p.f0.z.y >= 0.0f;
         faithful_wave = ps.faithful && lanes(!faithful_lane) == 0;
-        if (faithful_wave)
+        if (CULL && faithful_wave && ps.faithful == 2)
+            faithful_wave = wave_light_terms(lights, ps, wb, cull_enabled) <= kFaithfulMaxTerms;
+        const bool lean_wave = lanes(!lean_lane) == 0;
+        if (faithful_wave && lean_wave)
             d2 = lighting_fast<CULL, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
-        else if (lanes(!lean_lane) == 0)
+        else if (faithful_wave)
+            d2 = lighting_fast<CULL, false, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+        else if (lean_wave)
             d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
         else
             d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);

@@ -33,9 +33,9 @@ def shade(ctx, gb, pc, env):
     return out.cpu().numpy()
 
 
-# cfg4's normal-mapped material plane has waves outside the lean conditions (|N|^2 > 1 + 2^-20, zero F0
-# components), which stay on the exact loop: the mode need not show there.
-@pytest.mark.parametrize("cid,size,row_step,active", [(2, None, 1, True), (3, None, 8, True), (4, None, 8, False),
+# cfg4: 256 lights under tiled culling (each wave counts its ~5 surviving terms against the bound's 64)
+# on a normal-mapped material plane (the faithful loop's non-lean variant).
+@pytest.mark.parametrize("cid,size,row_step,active", [(2, None, 1, True), (3, None, 8, True), (4, None, 8, True),
                                                       (3, (1024, 128), 1, True)])
 def test_faithful_config_within_tolerance(cid, size, row_step, active, shading_ctx, gpu):
     cfg = S.CONFIGS[cid] if size is None else S.CONFIGS[cid].with_size(*size)
@@ -73,7 +73,8 @@ def test_faithful_golden_vectors(name, shading_ctx, gpu, env_map):
     assert np.array_equal(np.isnan(got), np.isnan(expected))
 
 
-@pytest.mark.parametrize("case", ["negative_strength", "negative_ambient", "exact_only", "65_lights"])
+@pytest.mark.parametrize("case", ["negative_strength", "negative_ambient", "exact_only", "65_lights",
+                                  "culled_100_lights_in_range"])
 def test_faithful_preconditions_keep_the_pass_exact(case, shading_ctx, gpu):
     """Where a light term could be negative (strength, ambient) or the sum is longer than the bound
     allows (> 64 lights) the error bound does not hold: the host turns the mode off and the frame
@@ -83,6 +84,8 @@ def test_faithful_preconditions_keep_the_pass_exact(case, shading_ctx, gpu):
     cfg = S.CONFIGS[2].with_size(512, 64)
     if case == "65_lights":
         cfg = dataclasses.replace(cfg, n_lights=65)
+    if case == "culled_100_lights_in_range":  # every wave keeps all 100 lights: > 64 summed terms
+        cfg = dataclasses.replace(cfg, n_lights=100, flags=N.PBR_FLAG_TILED_CULLING)
     planes, _ = S.fill_gbuffer_host(cfg)
     pc = S.scene_pass(cfg)
     if case == "negative_strength":
