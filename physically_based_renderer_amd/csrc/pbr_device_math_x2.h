@@ -280,6 +280,22 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
 __device__ __forceinline__ v2 rcp_hw(v2 y) { return v2{__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)}; }
 constexpr float kInvPi = 0x1.45f306p-2f;  // RN(1/kPi)
 
+// Fresnel x^5 of the faithful loop: compensated fp32 arithmetic in packed form (x^2 and x2^2 split exactly
+// by FMA, the cross term 2 x2 e2 folded in, one final rounding) -- within 2^-45 of x^5 before rounding,
+// so within 0.5 ulp + 2^-22 ulp of it and at most 1 ulp from glibc's powf (0.82 ulp), the same residue
+// the exact mode's fp64 x^5 has (pow5_light; DESIGN.md §2 counts it). 8 packed ops per pair instead of
+// 10 fp64 ones. The grazing band x > 0.99, where 1 - F cancels, keeps glibc's algorithm bit for bit.
+__device__ __forceinline__ v2 pow5_faithful(v2 x) {
+    const v2 x2 = x * x;
+    const v2 e2 = vfma(x, x, -x2);
+    const v2 x4 = x2 * x2;
+    const v2 t = vfma(x2 + x2, e2, vfma(x2, x2, -x4));
+    v2 p = vfma(x4, x, t * x);
+    if (__builtin_expect(x.x > PBR_POW5_GLIBC_FROM, 0)) p.x = pow5_glibc(x.x);
+    if (__builtin_expect(x.y > PBR_POW5_GLIBC_FROM, 0)) p.y = pow5_glibc(x.y);
+    return p;
+}
+
 struct Faithful2 {
     v2 a2gv;     // a^2 * GeometrySchlickGGX(N.V)
     f3x2 mabpi;  // (1 - metallic) * albedo / PI
@@ -306,7 +322,7 @@ __device__ __forceinline__ void brdf_faithful_x2(const PixelInvariants2& q, cons
     // absorbs; the clamp rides on the dot's last add.
     const v2 n_dot_l = LEAN ? dot3_sat(q.n, l) : vmax(dot3(q.n, l), splat(0.0f));
     const v2 r = rcp_hw((den * (n_dot_l * q.one_minus_k + q.k)) * (q.four_n_dot_v * n_dot_l + 0.001f));
-    const v2 p = pow5_light(1.0f - dot3_sat(h, q.v));
+    const v2 p = pow5_faithful(1.0f - dot3_sat(h, q.v));
     const f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
     const v2 kr = (fi.a2gv * n_dot_l) * r;
     const v2 w = att * n_dot_l;
