@@ -85,15 +85,16 @@ def _read_dump(path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cid,size,bands,output", [
-    (2, None, 1, "rgba32f"),          # config 2 at full size
-    (3, (480, 272), 3, "rgba32f"),    # 64 point lights + IBL, shaded as three row bands
-    (4, (640, 360), 2, "rgba8"),      # tiled culling + F0 plane into the RGBA8 back buffer
+@pytest.mark.parametrize("cid,size,bands,output,mode", [
+    (2, None, 1, "rgba32f", "exact"),        # config 2 at full size
+    (3, (480, 272), 3, "rgba32f", "exact"),  # 64 point lights + IBL, shaded as three row bands
+    (4, (640, 360), 2, "rgba8", "exact"),    # tiled culling + F0 plane into the RGBA8 back buffer
+    (3, (480, 272), 2, "rgba32f", "faithful"),  # the tolerance mode through the C++ interface
 ])
-def test_native_frame_equals_oracle(driver, tmp_path, gpu, cid, size, bands, output):
+def test_native_frame_equals_oracle(driver, tmp_path, gpu, cid, size, bands, output, mode):
     cfg = S.CONFIGS[cid] if size is None else S.CONFIGS[cid].with_size(*size)
     dump = str(tmp_path / "frame.bin")
-    args = ["--config", cid, "--bands", bands, "--output", output, "--dump", dump]
+    args = ["--config", cid, "--bands", bands, "--output", output, "--mode", mode, "--dump", dump]
     if size is not None:
         args += ["--width", size[0], "--height", size[1]]
     r = run(driver, *args)
@@ -116,8 +117,9 @@ def test_native_frame_equals_oracle(driver, tmp_path, gpu, cid, size, bands, out
 
 
 @pytest.mark.gpu
-def test_native_timed_run(driver, gpu):
-    r = run(driver, "--config", "3", "--steps", "10", "--warmup", "2", "--ramp-ms", "50")
+@pytest.mark.parametrize("mode", ["exact", "faithful"])
+def test_native_timed_run(driver, gpu, mode):
+    r = run(driver, "--config", "3", "--steps", "10", "--warmup", "2", "--ramp-ms", "50", "--mode", mode)
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["steps"] == 10 and d["value"] > 1000.0  # north-star floor: 10^9 shaded px/s
