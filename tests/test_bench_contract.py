@@ -1,0 +1,70 @@
+"""bench.py's measurement model on the CPU (no GPU): algorithmic bytes and FLOPs per pixel,
+the compute-vs-HBM roof choice, the PMC lookup keyed by workload and mode, and the CPU baseline leg
+(the reference's own shader build when present, else the C port) with its parity check."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+import bench
+from physically_based_renderer_amd import _native as N
+from physically_based_renderer_amd import scenes as S
+
+
+def test_bytes_per_pixel_follows_the_planes_read():
+    pc3 = S.scene_pass(S.CONFIGS[3])
+    assert bench.bytes_per_pixel(pc3) == 60            # 11 planes + RGBA fp32
+    assert bench.bytes_per_pixel(pc3, 4) == 48         # RGBA8 back buffer
+    pc4 = S.scene_pass(S.CONFIGS[4])
+    assert pc4.flags & N.PBR_FLAG_F0_PLANE
+    assert bench.bytes_per_pixel(pc4) == 72            # + F0 plane
+
+
+def test_flops_per_pixel_and_the_roof():
+    pc3 = S.scene_pass(S.CONFIGS[3])
+    f3 = bench.flops_per_pixel(pc3)
+    assert f3 == 27 + 20 + 91 * 64 + 87 == 5958
+    # config 3 sits right of the ridge (compute roof), config 2 left of it (HBM roof)
+    ridge = bench.FP32_PEAK_TFLOPS * 1e12 / (bench.HBM_PEAK_GBPS * 1e9)
+    assert f3 / bench.bytes_per_pixel(pc3) > ridge
+    pc2 = S.scene_pass(S.CONFIGS[2])
+    assert bench.flops_per_pixel(pc2) / bench.bytes_per_pixel(pc2) < ridge
+    # tiled culling counts the surviving lights, plus each light's range test once per culling tile
+    pc4 = S.scene_pass(S.CONFIGS[4])
+    f4 = bench.flops_per_pixel(pc4, lights_per_tile=5.0, tile_px=128)
+    assert f4 == pytest.approx(47 + 91 * 5.0 + 9 * 256 / 128)
+
+
+def test_pmc_lookup_is_keyed_by_workload_and_mode():
+    summary = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+    for key in ("cfg3_3840x2160_64pt_ibl_chelsea", "cfg3_3840x2160_64pt_ibl_chelsea_faithful"):
+        assert key in summary
+        traffic, busy = bench.load_pmc(key)
+        e = summary[key]
+        assert traffic == e["hbm_bytes_per_launch"] and 0.5 < busy <= 1.0
+        # HBM traffic within 10 % of the algorithmic bytes: no re-reads
+        assert 0.95 < e["traffic_over_algorithmic"] < 1.10
+        # the committed kernel trace agrees with the bench's own events within 2 %
+        kt = e["kernel_trace"]
+        assert abs(kt["mean_ms_timed_steps"] - kt["bench_avg_launch_ms"]) / kt["bench_avg_launch_ms"] < 0.02
+    assert bench.load_pmc("no_such_workload") == (None, None)
+
+
+@pytest.mark.parametrize("kind", ["auto", "port"])
+def test_cpu_baseline_leg_checks_parity(kind):
+    from oracle import oracle as O
+
+    cfg = S.CONFIGS[3].with_size(256, 16)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    env = S.env_map()
+    ops = O.OraclePass(eye=tuple(pc.eye_pos_w), ambient=tuple(pc.ambient_light), fresnel_r0=tuple(pc.fresnel_r0),
+                       opacity=pc.opacity, n_point=pc.num_point_lights, ambient_mode=pc.ambient_mode)
+    frame = O.shade(list(planes), ops, pc.light_array(), env, n_threads=4)  # stands in for the GPU frame
+    cpu, max_rel, exact, (step, ref) = bench.cpu_baseline(cfg, planes, pc, env, frame, 0, kind)
+    assert cpu["kind"] == ("reference" if kind == "auto" and O.ref_available() else "port")
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["single_thread_value"] > 0
+    assert max_rel == 0.0 and exact == 1.0 and step == 1
+    assert np.array_equal(ref.view(np.uint32), frame.view(np.uint32))
