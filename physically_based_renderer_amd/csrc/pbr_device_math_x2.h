@@ -267,16 +267,23 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
 // at grazing angles. Rearranged, with the error bounded instead of bit-matched: the well-conditioned
 // rest of BRDFCookTorrance and the attenuation,
 //
-//   spec.c = NDF * G * F.c / denom = F.c * (a^2 * G1(N.V) * N.L) / (den * (N.L (1-k) + k) * denom)
+//   spec.c = NDF * G * F.c / denom = F.c * (a^2 * G1(N.V) * N.L / PI) / (inner^2 * (N.L (1-k) + k) * denom)
 //   diff.c = (1 - F.c) * (1 - metallic) * albedo.c / PI
 //   sum.c += (diff.c + spec.c) * strength.c * (att * N.L),     att = min(RN(1/dist)^2, 1/0.01^2)
 //
-// with one hardware reciprocal (<= 1 ulp) for the three denominators, the per-pixel products
-// a^2 * G1(N.V) and (1 - metallic) * albedo / PI hoisted out of the loop, and fused multiply-adds
-// (single roundings) for the diffuse term, the diffuse + specular sum and the accumulation. Each light's
-// term stays within 38 roundings (2^-24 each) of the reference's; with every term >= 0 (host: strengths,
-// ambient, env texels >= 0, <= 64 lights; per wave: albedo >= 0, F0 in [0, 1]) the output is within
-// 5.9e-6 relative with the faithful finish -- inside the north-star 1e-5 -- but not bit-identical.
+// (inner = N.H^2 (a^2 - 1) + 1, the GGX denominator before its PI and square) with one hardware
+// reciprocal (<= 1 ulp) for the three denominators, the per-pixel products a^2 * G1(N.V) / PI and
+// (1 - metallic) * albedo / PI hoisted out of the loop, and fused multiply-adds (single roundings) for the
+// Smith and specular denominators, the diffuse term, the diffuse + specular sum and the accumulation.
+// Untiled passes run the loop on invariants rescaled by powers of two (faithful_scale): N / 4, so that
+// max(N.H, 0) and max(N.L, 0) come out / 4 and, in lean waves, ride on the dot's clamp bit instead of a
+// v_max per element -- exactly, because the fast window keeps every product of those dots 0 or >= 2^-110 --
+// with the 4s folded back into the other per-pixel factors; each light's term then stays within 26
+// roundings (2^-24 each) of the reference's. Tiled passes keep the first form (PI * inner^2, the reference's
+// roundings of the two denominators, N.L saturated in lean waves): within 38 roundings. With every term >= 0
+// (host: strengths, ambient, env texels >= 0, <= 64 summed terms; per wave: albedo >= 0, F0 in [0, 1]) the
+// output is within 5.5e-6 (untiled) / 5.9e-6 (tiled) relative with the faithful finish --
+// inside the north-star 1e-5 -- but not bit-identical.
 __device__ __forceinline__ v2 rcp_hw(v2 y) { return v2{__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)}; }
 constexpr float kInvPi = 0x1.45f306p-2f;  // RN(1/kPi)
 
@@ -296,50 +303,78 @@ __device__ __forceinline__ v2 pow5_faithful(v2 x) {
     return p;
 }
 
+// SCALED (the untiled kernels): the loop runs on invariants rescaled by powers of two (faithful_scale) and
+// the Smith and specular denominators are FMAs. Unscaled (tiled culling, where a wave sums a handful of
+// lights and the per-pixel rescaling does not pay for itself; measured 4% slower on config 4) keeps the
+// first form: N.L saturated in lean waves, PI * inner^2, the two denominators as the reference rounds them.
 struct Faithful2 {
-    v2 a2gv;     // a^2 * GeometrySchlickGGX(N.V)
-    f3x2 mabpi;  // (1 - metallic) * albedo / PI
+    v2 a2gv;     // a^2 * GeometrySchlickGGX(N.V), SCALED: * 16 / PI (4 for N.L / 4, 4 for the scaled sum)
+    f3x2 mabpi;  // (1 - metallic) * albedo / PI, SCALED: * 4
 };
+constexpr float kInvPi4 = 4.0f * kInvPi, kInvPi16 = 16.0f * kInvPi;  // exact scalings of RN(1/kPi)
+template <bool SCALED>
 __device__ __forceinline__ Faithful2 make_faithful(const PixelInvariants2& q) {
-    return Faithful2{q.a_sqr * q.ggx_v, f3x2{(q.one_minus_metal * q.albedo.x) * kInvPi,
-                                            (q.one_minus_metal * q.albedo.y) * kInvPi,
-                                            (q.one_minus_metal * q.albedo.z) * kInvPi}};
+    const float c = SCALED ? kInvPi4 : kInvPi;
+    return Faithful2{SCALED ? (q.a_sqr * q.ggx_v) * kInvPi16 : q.a_sqr * q.ggx_v,
+                     f3x2{(q.one_minus_metal * q.albedo.x) * c, (q.one_minus_metal * q.albedo.y) * c,
+                          (q.one_minus_metal * q.albedo.z) * c}};
 }
 
-// BRDFCookTorrance * radiance * N.L added into `sum`; `att` = the light's attenuation (1 for
-// directional lights), already 0 for lanes beyond the range. LEAN as in brdf_x2: outside lean waves
-// (|N| up to the window's bound, zero F0 components) `den` is tested against [2^-60, 2^60] so that the
-// product of the three denominators stays normal, and N.L keeps its max(., 0).
-template <bool LEAN>
+// The SCALED loop's invariants: N / 4, 16 (a^2 - 1), 4 (1 - k), 16 N.V. Every factor is a power of two and
+// every value is 0 or normal far from both ends in the fast window (normal components 0 or in [2^-20, 16],
+// a^2 - 1 in [-1, 0] with |a^2 - 1| 0 or >= 2^-24, 1 - k in [1/2, 7/8], N.V 0 or >= 2^-100), so scaling is
+// exact and faithful_unscale restores the bits the exact re-pass and the finish read. With V + L components
+// 0 or >= 2^-88 (and L/d >= 2^-65) the products of N/4 . H and N/4 . L stay 0 or >= 2^-110: no subnormal
+// rounding anywhere in those dots, so each is exactly a quarter of the reference's dot.
+__device__ __forceinline__ void faithful_scale(PixelInvariants2& q) {
+    q.n = f3x2{q.n.x * 0.25f, q.n.y * 0.25f, q.n.z * 0.25f};
+    q.a_sqr_minus_1 *= 16.0f;
+    q.one_minus_k *= 4.0f;
+    q.four_n_dot_v *= 4.0f;
+}
+__device__ __forceinline__ void faithful_unscale(PixelInvariants2& q) {
+    q.n = f3x2{q.n.x * 4.0f, q.n.y * 4.0f, q.n.z * 4.0f};
+    q.a_sqr_minus_1 *= 0.0625f;
+    q.one_minus_k *= 0.25f;
+    q.four_n_dot_v *= 0.25f;
+}
+
+// BRDFCookTorrance * radiance * N.L added into `sum`; `att` = the light's attenuation (1 for directional
+// lights), already 0 for lanes beyond the range. LEAN as in brdf_x2: outside lean waves (|N| up to the
+// window's bound, zero F0 components) N.H and N.L take max(., 0) (no clamp bit: their quarter may exceed
+// 1), and the GGX denominator is tested so that the product of the three denominators stays normal.
+template <bool LEAN, bool SCALED>
 __device__ __forceinline__ void brdf_faithful_x2(const PixelInvariants2& q, const Faithful2& fi, float4 s, v2 att,
                                                  f3x2 l, f3x2 h, m2& ok, f3x2& sum) {
-    const v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
-    v2 den = ((n_dot_h * n_dot_h) * q.a_sqr_minus_1 + 1.0f);  // exact: the ill-conditioned GGX denominator
-    den = kPi * den * den;
-    if (!LEAN) ok &= ge(den, 0x1p-60f) & le(den, 0x1p60f);
-    // Lean waves: saturate instead of max(., 0). N.L is not on the ill-conditioned chain, and there it
-    // exceeds 1 by at most 2^-20.6 (|N|^2 <= 1 + 2^-20, |L| <= 1 + 2^-23), a relative change the bound
-    // absorbs; the clamp rides on the dot's last add.
+    // SCALED: max(N.H, 0) / 4 and max(N.L, 0) / 4, bit for bit. Lean waves: |N|, |H|, |L| <= 1 + 2^-19.6, so
+    // the quarter is below 1 and the [0, 1] clamp of the dot's last add is max(., 0). Unscaled lean waves
+    // saturate N.L instead of max(., 0): N.L is not on the ill-conditioned chain, and there it exceeds 1 by
+    // at most 2^-20.6, a relative change the bound absorbs.
+    const v2 n_dot_h = (SCALED && LEAN) ? dot3_sat(q.n, h) : vmax(dot3(q.n, h), splat(0.0f));
+    const v2 inner = ((n_dot_h * n_dot_h) * q.a_sqr_minus_1 + 1.0f);  // exact: the ill-conditioned GGX denominator
+    const v2 den = SCALED ? inner * inner : kPi * inner * inner;      // SCALED: the NDF's denominator / PI
+    if (!LEAN) ok &= SCALED ? ge(den, 0x1p-62f) & le(den, 0x1p58f) : ge(den, 0x1p-60f) & le(den, 0x1p60f);
     const v2 n_dot_l = LEAN ? dot3_sat(q.n, l) : vmax(dot3(q.n, l), splat(0.0f));
-    const v2 r = rcp_hw((den * (n_dot_l * q.one_minus_k + q.k)) * (q.four_n_dot_v * n_dot_l + 0.001f));
+    const v2 r = SCALED ? rcp_hw((den * vfma(n_dot_l, q.one_minus_k, q.k)) * vfma(q.four_n_dot_v, n_dot_l, splat(0.001f)))
+                        : rcp_hw((den * (n_dot_l * q.one_minus_k + q.k)) * (q.four_n_dot_v * n_dot_l + 0.001f));
     const v2 p = pow5_faithful(1.0f - dot3_sat(h, q.v));
     const f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
-    const v2 kr = (fi.a2gv * n_dot_l) * r;
-    const v2 w = att * n_dot_l;
+    const v2 kr = (fi.a2gv * n_dot_l) * r;  // SCALED: 4 x the specular factor
+    const v2 w = att * n_dot_l;             // SCALED: att * N.L / 4
     sum.x = vfma(vfma(kr, f.x, vfma(-f.x, fi.mabpi.x, fi.mabpi.x)), s.x * w, sum.x);
     sum.y = vfma(vfma(kr, f.y, vfma(-f.y, fi.mabpi.y, fi.mabpi.y)), s.y * w, sum.y);
     sum.z = vfma(vfma(kr, f.z, vfma(-f.z, fi.mabpi.z, fi.mabpi.z)), s.z * w, sum.z);
 }
 
-template <bool LEAN>
+template <bool LEAN, bool SCALED>
 __device__ __forceinline__ void directional_faithful_x2(const PixelInvariants2& q, const Faithful2& fi, float4 s,
                                                         float4 d, m2& ok, f3x2& sum) {
     const f3x2 l = splat3(-d.x, -d.y, -d.z);
     const f3x2 h = normalize_x2(add3(q.v, l), ok);
-    brdf_faithful_x2<LEAN>(q, fi, s, splat(1.0f), l, h, ok, sum);
+    brdf_faithful_x2<LEAN, SCALED>(q, fi, s, splat(1.0f), l, h, ok, sum);
 }
 
-template <bool SPOT, bool LEAN>
+template <bool SPOT, bool LEAN, bool SCALED>
 __device__ __forceinline__ void point_or_spot_faithful_x2(const PixelInvariants2& q, const Faithful2& fi,
                                                           const f3x2& pos, float4 s, float4 d, float4 p, m2& ok,
                                                           f3x2& sum) {
@@ -360,7 +395,7 @@ __device__ __forceinline__ void point_or_spot_faithful_x2(const PixelInvariants2
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
     att = vsel(lit, att, splat(0.0f));  // beyond the range: +0 (see point_or_spot_x2)
-    brdf_faithful_x2<LEAN>(q, fi, s, att, l, h, ok, sum);
+    brdf_faithful_x2<LEAN, SCALED>(q, fi, s, att, l, h, ok, sum);
 }
 
 }  // namespace pbr

@@ -178,12 +178,12 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
                                               const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total) {
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     Faithful2 fi{};
-    if (FAITHFUL) fi = make_faithful(q);
+    if (FAITHFUL) fi = make_faithful<!CULL>(q);
     for (int j = 0; j < ps.n_dir; ++j) {  // directional: never culled
         const LightRec r = light_rec(lights, j);
         m2 ok = fast_ok & light_flag(r);
         if (FAITHFUL) {
-            directional_faithful_x2<LEAN>(q, fi, r.s, r.d, ok, direct);
+            directional_faithful_x2<LEAN, !CULL>(q, fi, r.s, r.d, ok, direct);
         } else {
             const f3x2 c = directional_x2<LEAN>(q, r.s, r.d, ok);
             direct = add3(direct, c);  // shadowFactor (1,1,1) * c == c
@@ -201,7 +201,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
             // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation)
             // when inside the window, and every lane outside it is redone.
             if (FAITHFUL) {
-                point_or_spot_faithful_x2<SPOT, LEAN>(q, fi, pos, r.s, r.d, r.p, ok, direct);
+                point_or_spot_faithful_x2<SPOT, LEAN, !CULL>(q, fi, pos, r.s, r.d, r.p, ok, direct);
             } else {
                 m2 lit;
                 const f3x2 c = point_or_spot_x2<SPOT, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         const f3 v0 = va_ok ? lane(v, 0) : normalize3(lane(ve, 0)), v1 = vb_ok ? lane(v, 1) : normalize3(lane(ve, 1));
         v = f3x2{v2{v0.x, v1.x}, v2{v0.y, v1.y}, v2{v0.z, v1.z}};
     }
-    const PixelInvariants2 q2 = make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness, fast2);
+    PixelInvariants2 q2 = make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness, fast2);
 
     // The wave's world-space box (its 64x2 pixels; background pixels excluded): wave64 butterflies,
     // then scalar registers. Non-finite positions disable culling for the wave (the reference's
@@ -503,11 +503,16 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         if (CULL && faithful_wave && ps.faithful == 2)
             faithful_wave = wave_light_terms(lights, ps, wb, cull_enabled) <= kFaithfulMaxTerms;
         const bool lean_wave = lanes(!lean_lane) == 0;
-        if (faithful_wave && lean_wave)
+        // Untiled faithful waves read rescaled invariants (exact both ways, faithful_scale).
+        if (faithful_wave && lean_wave) {
+            if (!CULL) faithful_scale(q2);
             d2 = lighting_fast<CULL, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
-        else if (faithful_wave)
+            if (!CULL) faithful_unscale(q2);
+        } else if (faithful_wave) {
+            if (!CULL) faithful_scale(q2);
             d2 = lighting_fast<CULL, false, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
-        else if (lean_wave)
+            if (!CULL) faithful_unscale(q2);
+        } else if (lean_wave)
             d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
         else
             d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
