@@ -3,6 +3,9 @@
 * fastdiv_probe.hip -- v_rcp_f32 + one Newton step is RN(1/b) for every b with exponent in
   [-64, 64] (the window the fast path admits), and the Markstein quotient equals IEEE a / b on
   random operands inside the window;
+* quarter_dot_probe.hip -- the faithful loop's power-of-two rescaled invariants (faithful_scale): N/4 . H
+  is exactly N.H / 4 in the fast window, so the dot's clamp bit gives max(N.H, 0) / 4 in lean waves, the
+  GGX denominator keeps the reference's bits, and faithful_unscale restores every invariant;
 * libm_probe.hip -- the device build of libm_f32.h (WorldToSkyUV's atan2f / asinf) returns the host
   glibc's bits: asinf on every float in [-1, 1], atanf on every finite float, and 2^27 random
   atan2f pairs.
@@ -26,7 +29,7 @@ FLAGS = ["-O3", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result", "-fPIC"
 def probes(tmp_path_factory, gpu):
     d = tmp_path_factory.mktemp("probes")
     libs = {}
-    for name in ("fastdiv_probe", "libm_probe", "sqrt_probe", "gamma_probe"):
+    for name in ("fastdiv_probe", "libm_probe", "sqrt_probe", "gamma_probe", "quarter_dot_probe"):
         so = str(d / f"{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, os.path.join(ROOT, "tests", "hip", f"{name}.hip"), "-o", so,
                         "-lpthread"], check=True)
@@ -105,3 +108,17 @@ def test_faithful_gamma_error_exhaustive(probes):
             assert out[e - lo] <= 5.4e-7, e
         else:
             assert out[e - lo] == 0.0, e
+
+
+@pytest.mark.parametrize("lean", [1, 0])
+def test_faithful_quarter_dots_are_exact(probes, lean):
+    """faithful_scale's claim (pbr_device_math_x2.h): over 2^24 random pixel pairs in the fast window --
+    H near N (N.H ~ 1, where the GGX denominator cancels), components forced to 0 or to the window's small
+    ends -- the rescaled dot is the reference's dot / 4 bit for bit (clamp bit in lean waves, max
+    elsewhere), the GGX denominator from it has the reference's bits, and unscaling is exact."""
+    L = probes["quarter_dot_probe"]
+    bad = (ctypes.c_ulonglong * 4)()
+    assert L.probe_quarter_dots(ctypes.c_ulonglong(0x9A4D + lean), 4096, 16, lean, bad) == 0
+    assert list(bad[:3]) == [0, 0, 0]
+    if lean:  # control: the samples reach N.H > 1, where saturating the unscaled dot would have clamped
+        assert bad[3] > 0
