@@ -374,27 +374,39 @@ __device__ __forceinline__ void directional_faithful_x2(const PixelInvariants2& 
     brdf_faithful_x2<LEAN, SCALED>(q, fi, s, splat(1.0f), l, h, ok, sum);
 }
 
+// The range test of ComputePointLight (LightingUtil.hlsl:131: d > 100 adds nothing) as a factor of exactly
+// 1 or 0: floats next to 100 are 2^-17 apart, so d <= 100 <=> 2^17 (100 + 2^-17 - d) >= 1 and d > 100 <=> it
+// is <= 0. One v_pk_fma forms that product with a single rounding (-2^17 d is exact, 2^17 (100 + 2^-17) =
+// 13107201 is a float) and its clamp bit maps it to 1 or 0 (NaN to 0: such a lane fails the window). Both
+// constants come from one SGPR pair (op_sel picks the half: one constant-bus read). Replaces the two
+// compares and two selects of the lit mask. s_nop pads as in dot3_sat.
+__device__ __forceinline__ v2 in_range01(v2 dist) {
+    const v2 kc = v2{-0x1p17f, 13107201.0f};
+    v2 r;
+    asm("s_nop 1\n\tv_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\ts_nop 1"
+        : "=v"(r) : "v"(dist), "s"(kc));
+    return r;
+}
+
 template <bool SPOT, bool LEAN, bool SCALED>
 __device__ __forceinline__ void point_or_spot_faithful_x2(const PixelInvariants2& q, const Faithful2& fi,
                                                           const f3x2& pos, float4 s, float4 d, float4 p, m2& ok,
                                                           f3x2& sum) {
     f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
     const v2 dist = sqrt_nr(dot3(l, l));
-    const m2 lit = not_gt(dist, kLightRange);
-    ok &= ge(dist, 0x1p-20f);
+    // Window: dist >= 0.01 (stricter than the exact loop's 2^-20). Then max(dist, 0.01) of CalcAttenuation
+    // (LightingUtil.hlsl:35-40) is dist itself and the attenuation is RN(1/dist)^2 from the correctly rounded
+    // reciprocal the exact L already needs; a pixel closer than 0.01 to a light is redone exactly.
+    ok &= ge(dist, 0.01f);
     const Recip2 rdist = recip_nr(dist);
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     const f3x2 h = normalize_x2(add3(q.v, l), ok);
-    // 1 / max(dist, 0.01)^2 (LightingUtil.hlsl:35-40) from the correctly rounded RN(1/dist) the exact L
-    // already needs: dist >= 0.01 <=> RN(1/dist) <= 100, so the clamp is a min against the constant.
-    constexpr float kAttMax = 1.0f / (0.01f * 0.01f);
     v2 att = rdist.r * rdist.r;
-    att = v2{fminf(att.x, kAttMax), fminf(att.y, kAttMax)};
     if (SPOT) {
         const v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
-    att = vsel(lit, att, splat(0.0f));  // beyond the range: +0 (see point_or_spot_x2)
+    att *= in_range01(dist);  // beyond the range: +0 (see point_or_spot_x2)
     brdf_faithful_x2<LEAN, SCALED>(q, fi, s, att, l, h, ok, sum);
 }
 
