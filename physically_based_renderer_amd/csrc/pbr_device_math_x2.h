@@ -234,18 +234,31 @@ __device__ __forceinline__ v2 max_dsat(v2 dist) {
               __builtin_amdgcn_fmed3f(dist.y, 0.01f, 0x1p100f)};
 }
 
-// ComputePointLight / ComputeSpotLight, packed fast path. `lit` = the range test passed (exact,
-// as in the scalar version). For a lane with lit == 0 the attenuation is set to +0, so the returned
-// contribution is (finite) * 0 = +-0 whenever the lane is inside the window (`ok`: every value of the
-// fast path is then finite; pbr_set_pass clears the light's window flag when its strength is not
-// finite), and adding +-0 to the running sum is the identity the reference's skipped light is. Lanes
-// outside the window are redone by the caller whether lit or not.
+// The range test of ComputePointLight (LightingUtil.hlsl:131: d > 100 adds nothing) as a factor of exactly
+// 1 or 0: floats next to 100 are 2^-17 apart, so d <= 100 <=> 2^17 (100 + 2^-17 - d) >= 1 and d > 100 <=> it
+// is <= 0. One v_pk_fma forms that product with a single rounding (-2^17 d is exact, 2^17 (100 + 2^-17) =
+// 13107201 is a float) and its clamp bit maps it to 1 or 0 (NaN to 0: such a lane fails the window). Both
+// constants come from one SGPR pair (op_sel picks the half: one constant-bus read). Replaces the two
+// compares and two selects of a lit mask. s_nop pads as in dot3_sat.
+__device__ __forceinline__ v2 in_range01(v2 dist) {
+    const v2 kc = v2{-0x1p17f, 13107201.0f};
+    v2 r;
+    asm("s_nop 1\n\tv_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\ts_nop 1"
+        : "=v"(r) : "v"(dist), "s"(kc));
+    return r;
+}
+
+// ComputePointLight / ComputeSpotLight, packed fast path. The range test (exact, as in the scalar
+// version) scales the attenuation by 1 or 0 (in_range01), so an unlit lane's contribution is
+// (finite) * 0 = +-0 whenever the lane is inside the window (`ok`: every value of the fast path is then
+// finite; pbr_set_pass clears the light's window flag when its strength is not finite), and adding +-0
+// to the running sum is the identity the reference's skipped light is. Lanes outside the window are
+// redone by the caller whether lit or not.
 template <bool SPOT, bool LEAN>
 __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, const f3x2& pos,
-                                                 float4 s, float4 d, float4 p, m2& lit, m2& ok) {
+                                                 float4 s, float4 d, float4 p, m2& ok) {
     f3x2 l = f3x2{p.x - pos.x, p.y - pos.y, p.z - pos.z};
     v2 dist = sqrt_nr(dot3(l, l));
-    lit = not_gt(dist, kLightRange);
     ok &= ge(dist, 0x1p-20f);
     const Recip2 rdist = recip_nr(dist);
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
@@ -256,7 +269,7 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
         v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
     }
-    att = vsel(lit, att, splat(0.0f));
+    att *= in_range01(dist);  // beyond the range: +0
     return brdf_x2<LEAN>(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
 }
 
@@ -372,20 +385,6 @@ __device__ __forceinline__ void directional_faithful_x2(const PixelInvariants2& 
     const f3x2 l = splat3(-d.x, -d.y, -d.z);
     const f3x2 h = normalize_x2(add3(q.v, l), ok);
     brdf_faithful_x2<LEAN, SCALED>(q, fi, s, splat(1.0f), l, h, ok, sum);
-}
-
-// The range test of ComputePointLight (LightingUtil.hlsl:131: d > 100 adds nothing) as a factor of exactly
-// 1 or 0: floats next to 100 are 2^-17 apart, so d <= 100 <=> 2^17 (100 + 2^-17 - d) >= 1 and d > 100 <=> it
-// is <= 0. One v_pk_fma forms that product with a single rounding (-2^17 d is exact, 2^17 (100 + 2^-17) =
-// 13107201 is a float) and its clamp bit maps it to 1 or 0 (NaN to 0: such a lane fails the window). Both
-// constants come from one SGPR pair (op_sel picks the half: one constant-bus read). Replaces the two
-// compares and two selects of the lit mask. s_nop pads as in dot3_sat.
-__device__ __forceinline__ v2 in_range01(v2 dist) {
-    const v2 kc = v2{-0x1p17f, 13107201.0f};
-    v2 r;
-    asm("s_nop 1\n\tv_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\ts_nop 1"
-        : "=v"(r) : "v"(dist), "s"(kc));
-    return r;
 }
 
 template <bool SPOT, bool LEAN, bool SCALED>

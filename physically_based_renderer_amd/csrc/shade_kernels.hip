@@ -203,8 +203,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
             if (FAITHFUL) {
                 point_or_spot_faithful_x2<SPOT, LEAN, !CULL>(q, fi, pos, r.s, r.d, r.p, ok, direct);
             } else {
-                m2 lit;
-                const f3x2 c = point_or_spot_x2<SPOT, LEAN>(q, pos, r.s, r.d, r.p, lit, ok);
+                const f3x2 c = point_or_spot_x2<SPOT, LEAN>(q, pos, r.s, r.d, r.p, ok);
                 direct = add3(direct, c);
             }
             redo |= ~ok;

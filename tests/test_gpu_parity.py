@@ -356,3 +356,37 @@ def test_ibl_near_poles_and_seam(shading_ctx, gpu, env_map):
         ref = O.shade(list(p), oracle_pass_from_constants(pc), None, env_map, n_threads=8)
         report(f"IBL poles/seam flags={flags}", got, ref)
         assert O.bit_equal(got, ref).all()
+
+
+@pytest.mark.parametrize("flags", [0, N.PBR_FLAG_FAITHFUL])
+def test_range_cut_at_100_on_gpu(flags, shading_ctx, gpu):
+    """`if (d > 100) return 0` (LightingUtil.hlsl:131) through the kernel's exact 0/1 range factor
+    (pbr_device_math_x2.h, in_range01): pixels 100 + k * 2^-17 from the light, k in [-8, 8), straddle the
+    cut. Exact mode: bit-identical to the oracle; faithful mode: within 1e-5, and every pixel the oracle
+    leaves unlit equals the no-light frame of the same mode."""
+    w = 16
+    p = np.zeros((O.NUM_PLANES, 1, w), np.float32)
+    p[0, 0, :] = -np.arange(-8, 8, dtype=np.float32) * np.float32(2.0 ** -17)  # l.x = 100 + k ulp(100)
+    p[3] = 1.0  # N faces +x, towards the light
+    p[6:9] = 0.5
+    p[10] = 0.5
+    p[11] = 1.0
+    lights = np.array([[1e4, 1e4, 1e4, 64.0, 0, 0, 1, 0, 100.0, 0, 0, 0]], np.float32)
+
+    def pass_with(n_point):
+        return PassConstants(eye_pos_w=(50.0, 0.0, -5.0), ambient_light=(0.03, 0.03, 0.03), num_point_lights=n_point,
+                             flags=flags, lights_array=lights if n_point else None)
+
+    pc = pass_with(1)
+    got = gpu_shade(shading_ctx, p, pc, None, gpu)
+    ref = O.shade(list(p), oracle_pass_from_constants(pc), pc.light_array())
+    base_ref = O.shade(list(p), oracle_pass_from_constants(pass_with(0)), None)
+    base_gpu = gpu_shade(shading_ctx, p, pass_with(0), None, gpu)
+    unlit = np.all(ref[0] == base_ref[0], axis=-1)
+    assert 0 < unlit.sum() < w  # both sides of the cut are present
+    if flags == 0:
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    else:
+        assert O.rel_err(got, ref).max() <= REL_TOL
+    assert np.array_equal(got[0, unlit].view(np.uint32), base_gpu[0, unlit].view(np.uint32))
+    assert not np.any(np.all(got[0, ~unlit] == base_gpu[0, ~unlit], axis=-1))
