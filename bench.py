@@ -92,7 +92,8 @@ def load_pmc(workload: str):
 
 def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int, kind: str = "auto"):
     """Time the reference CPU shader path on every k-th row of the frame (rank 0, N = 1) and check parity
-    there. kind "reference": the reference's own LightingUtil.hlsl compiled as C++ (oracle/_ref, built in
+    there. kind "reference": the reference's own pixel shader (Default.hlsl PS + Core.hlsl + LightingUtil.hlsl)
+    compiled as C++ (oracle/_ref, built in
     the build container; nothing under /root/reference is read at run time), one row band per host thread;
     kind "port": the C restatement oracle/pbr_oracle.c (pthreads). "auto" takes the reference build when
     it is present. Both are test infrastructure, used here only as the CPU baseline and the checker."""
@@ -139,7 +140,7 @@ def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int, kind: s
                 break
     except OSError:
         pass
-    what = ("oracle/_ref/libpbr_ref.so: the reference's LightingUtil.hlsl compiled as C++ (g++ -O2 "
+    what = ("oracle/_ref/libpbr_ref.so: the reference's Default.hlsl PS (+ Core/LightingUtil.hlsl) compiled as C++ (g++ -O2 "
             f"-ffp-contract=off), {n_threads} host threads over row bands" if use_ref else
             f"oracle/pbr_oracle.c, -O2 -ffp-contract=off, {n_threads} pthreads")
     return {

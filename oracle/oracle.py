@@ -1,7 +1,8 @@
 """oracle/oracle.py -- TEST INFRASTRUCTURE ONLY (ctypes front for the parity checker).
 
 Loads ``oracle/liboracle.so`` (plain-C restatement, pbr_oracle.c) or ``oracle/_ref/libpbr_ref.so``
-(the reference's own LightingUtil.hlsl compiled as C++, ref_harness.cpp). Only tests/,
+(the reference's own pixel-shader text -- Default.hlsl's PS with Core.hlsl and LightingUtil.hlsl, and
+Skybox.hlsl's PS -- compiled as C++: strip_hlsl.py + ref_harness.cpp). Only tests/,
 ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg may import this module; the product
 package never does.
 """
@@ -137,7 +138,7 @@ def shade(planes, opass: OraclePass, lights=None, env=None, n_threads: int = 1) 
 
 
 def shade_ref(planes, opass: OraclePass, lights=None, env=None) -> np.ndarray:
-    """The reference's LightingUtil.hlsl compiled as C++ (oracle/_ref); this container only."""
+    """The reference's Default.hlsl PS compiled as C++ (oracle/_ref); this container and the travelling build."""
     return _shade(_load(REF_SO, "ref_shade"), planes, opass, lights, env, 1)
 
 

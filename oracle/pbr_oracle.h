@@ -8,7 +8,8 @@
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
  * Parity is pinned: tests/golden/ holds vectors produced by oracle/_ref (the reference's own
- * LightingUtil.hlsl compiled as C++), and tests/test_oracle_golden.py checks this file against them.
+ * pixel-shader text -- Default.hlsl's PS with Core.hlsl and LightingUtil.hlsl, Skybox.hlsl's PS -- compiled
+ * as C++), and tests/test_oracle_golden.py checks this file against them.
  *
  * The oracle has its own flat interface (no product header), so a product bug in struct
  * marshalling cannot hide behind a shared definition.

@@ -1,18 +1,28 @@
 // oracle/ref_harness.cpp -- TEST INFRASTRUCTURE ONLY.  Built into oracle/_ref/libpbr_ref.so by
 // oracle/Makefile, and only where /root/reference exists (the build container). The built library reads
 // nothing from /root/reference at run time; it travels with the tree and serves bench.py's CPU baseline
-// (kind "reference"). Stateless: every entry point may run concurrently on disjoint row bands.
+// (kind "reference"). Entry points may run concurrently on disjoint row bands: all shader state
+// (cbuffers, bound textures) is thread_local.
 //
-// The reference's own light/BRDF code -- /root/reference/Source/Shaders/LightingUtil.hlsl, included
-// UNMODIFIED by absolute path -- compiled as C++ on top of hlsl_prelude.hpp. It is included once
-// per light-count permutation (the NUM_*_LIGHTS defines of Core.hlsl:1-12) so that the reference's
-// ComputeLighting (LightingUtil.hlsl:170-200) runs as shipped whenever the counts match a
-// permutation; other counts (beyond MAX_LIGHTS = 16, LightingUtil.hlsl:7) loop over the reference's
-// ComputeDirectionalLight / ComputePointLight / ComputeSpotLight in ComputeLighting's order.
+// What runs is the reference's own shader text:
+//   * the pixel shader PS, Default.hlsl:47-161, with its includes Core.hlsl (cbuffers, resources) and
+//     LightingUtil.hlsl (the BRDF, unmodified), after oracle/strip_hlsl.py's counted, syntax-only rewrite
+//     (generated into oracle/_ref/gen/, never committed);
+//   * the IBL_DIFFUSE ambient: the same PS with the author's commented-out block Default.hlsl:140-149
+//     re-enabled (Default_ibl.hlsl, same script);
+//   * the sky pass: Skybox.hlsl's PS (:37-49).
+// The only restated shading code left is the AO extension (ps_pixel_ao_extension below): the reference
+// has no AO term, so there is no reference text to compile for it.
 //
-// The pixel-shader composition (Default.hlsl:47-161: V, F0 resolve, ambient, tonemap, gamma) needs
-// texture/cbuffer syntax g++ cannot take, so those ~12 lines are restated below, each citing its line.
-// Output: golden vectors (tests/golden/gen_golden.py) that pin oracle/pbr_oracle.c.
+// Permutations (the D3D_SHADER_MACRO defines of PBRApp.cpp:715-754): DIFFUSE/METALLIC/ROUGHNESS/NORMAL
+// _TEXTURE = 1 with the G-buffer bound as the maps (ps_binding.inc explains the exact embedding),
+// SPECULAR_TEXTURE = 1 for the F0 plane (config 4) else 0 (F0 = lerp(g_FresnelR0, albedo, metallic)),
+// ALPHA_TEST = 0. The light counts NUM_DIR/POINT/SPOT_LIGHTS (Core.hlsl:1-12) are compile-time in the
+// reference; here they are runtime values behind macros whose preprocessor value is 1, so the
+// `#if (NUM_*_LIGHTS > 0)` guards of ComputeLighting (LightingUtil.hlsl:178, 185, 192) keep their loops
+// and each loop runs the pass's count (a loop with zero trips is what the #if removes). The shipped
+// default permutation (Core.hlsl's own 4/0/0, no defines) is compiled too and runs whenever a pass has
+// exactly those counts.
 #include <cstdint>
 #include <cstddef>
 #include <cmath>
@@ -20,54 +30,29 @@
 #include "hlsl_prelude.hpp"
 #include "pbr_oracle.h"
 
-#define PBR_REF_LIGHTINGUTIL "/root/reference/Source/Shaders/LightingUtil.hlsl"
+#define PBR_HLSL_GLOBAL thread_local
+#define PBR_ORACLE_MAX_LIGHTS 1024
 
 namespace hlsl {
-// Reference scene permutation: Core.hlsl defaults (4 directional, 0 point, 0 spot).
-namespace ref_d4 {
-#define NUM_DIR_LIGHTS 4
-#define NUM_POINT_LIGHTS 0
-#define NUM_SPOT_LIGHTS 0
-#include PBR_REF_LIGHTINGUTIL
-#undef NUM_DIR_LIGHTS
-#undef NUM_POINT_LIGHTS
-#undef NUM_SPOT_LIGHTS
-}  // namespace ref_d4
-namespace ref_p1 {
-#define NUM_DIR_LIGHTS 0
-#define NUM_POINT_LIGHTS 1
-#define NUM_SPOT_LIGHTS 0
-#include PBR_REF_LIGHTINGUTIL
-#undef NUM_DIR_LIGHTS
-#undef NUM_POINT_LIGHTS
-#undef NUM_SPOT_LIGHTS
-}  // namespace ref_p1
-namespace ref_p8 {
-#define NUM_DIR_LIGHTS 0
-#define NUM_POINT_LIGHTS 8
-#define NUM_SPOT_LIGHTS 0
-#include PBR_REF_LIGHTINGUTIL
-#undef NUM_DIR_LIGHTS
-#undef NUM_POINT_LIGHTS
-#undef NUM_SPOT_LIGHTS
-}  // namespace ref_p8
-namespace ref_mix {
-#define NUM_DIR_LIGHTS 4
-#define NUM_POINT_LIGHTS 8
-#define NUM_SPOT_LIGHTS 4
-#include PBR_REF_LIGHTINGUTIL
-#undef NUM_DIR_LIGHTS
-#undef NUM_POINT_LIGHTS
-#undef NUM_SPOT_LIGHTS
-}  // namespace ref_mix
 
-// Linear-wrap bilinear filter over an R16G16B16A16_UNORM texture (the D3D sampler g_SamLinearWrap,
-// PBRApp.cpp:1157-1162), in the fp32 form DESIGN.md fixes (hardware 8-bit sub-texel weights are not
-// reproducible: texture filtering parity is defined by this formula, not pinned to a GPU).
+struct SamplerState {};
+
+// A bound texture. Two kinds:
+//  * constant: the G-buffer view of a material map -- Sample returns the pixel's stored value;
+//  * bilinear: linear-wrap filtering over an RGBA texture (the sampler g_SamLinearWrap,
+//    PBRApp.cpp:1157-1162), in the fp32 form DESIGN.md fixes (hardware 8-bit sub-texel weights are not
+//    reproducible: texture-filtering parity is defined by this formula, not pinned to a GPU).
 struct Texture2D {
-    const uint16_t* texels;
-    int w, h;
-    const float* ftexels = nullptr;  // RGBA fp32 texture (HDR, or UNORM16 pre-decoded), used if set
+    float4 value;
+    const uint16_t* texels = nullptr;  // R16G16B16A16_UNORM texels (decoded as u16 / 65535)
+    const float* ftexels = nullptr;    // RGBA fp32 texels (HDR, or UNORM16 pre-decoded), used if set
+    int w = 0, h = 0;
+
+    static Texture2D constant(float r, float g, float b, float a) {
+        Texture2D t;
+        t.value = float4(r, g, b, a);
+        return t;
+    }
     static int wrap(float f, int n) {
         if (!(f == f) || f > 2.0e9f || f < -2.0e9f) return 0;
         int i = (int)f % n;
@@ -77,26 +62,22 @@ struct Texture2D {
         const size_t i = ((size_t)y * (size_t)w + (size_t)x) * 4u + (size_t)c;
         return ftexels ? ftexels[i] : (float)texels[i] / 65535.0f;
     }
-    float3 Sample(float3 uvw) const {  // only .xy is a coordinate (Default.hlsl:144)
-        float x = uvw.x * (float)w - 0.5f, y = uvw.y * (float)h - 0.5f;
+    float4 Sample(SamplerState, float2 uv) const {
+        if (!texels && !ftexels) return value;
+        float x = uv.x * (float)w - 0.5f, y = uv.y * (float)h - 0.5f;
         float x0f = std::floor(x), y0f = std::floor(y);
         float fx = x - x0f, fy = y - y0f;
         int x0 = wrap(x0f, w), y0 = wrap(y0f, h);
         int x1 = x0 + 1 == w ? 0 : x0 + 1, y1 = y0 + 1 == h ? 0 : y0 + 1;
-        float r[3];
-        for (int c = 0; c < 3; ++c)
+        float r[4];
+        for (int c = 0; c < 4; ++c)
             r[c] = lerp(lerp(fetch(x0, y0, c), fetch(x1, y0, c), fx), lerp(fetch(x0, y1, c), fetch(x1, y1, c), fx), fy);
-        return float3(r[0], r[1], r[2]);
+        return float4(r[0], r[1], r[2], r[3]);
     }
 };
-}  // namespace hlsl
-
-using namespace hlsl;
-
-namespace {
 
 template <class Light>
-void to_ref_light(const oracle_light& s, Light& d) {
+inline void pbr_to_ref_light(const oracle_light& s, Light& d) {
     d.Strength = float3(s.strength[0], s.strength[1], s.strength[2]);
     d.SpotPower = s.spot_power;
     d.Direction = float3(s.direction[0], s.direction[1], s.direction[2]);
@@ -105,114 +86,156 @@ void to_ref_light(const oracle_light& s, Light& d) {
     d.__PAD001 = 0.0f;
 }
 
-// ComputeLighting through the reference permutation NS when the counts match it exactly.
-template <int ND, int NP, int NS, class LightT, class MaterialT, class Fn>
-bool try_permutation(const oracle_pass& ps, const oracle_light* lights, const MaterialT& mat, float3 pos,
-                     float3 N, float3 V, float3& out, Fn compute_lighting) {
-    if (ps.n_dir != ND || ps.n_point != NP || ps.n_spot != NS) return false;
-    LightT g[16];
-    for (int i = 0; i < ND + NP + NS; ++i) to_ref_light(lights[i], g[i]);
-    out = compute_lighting(g, mat, pos, N, V, float3(1.0f));
-    return true;
-}
+// Runtime light counts (see the header comment). In an #if the identifiers evaluate to 0, so
+// PBR_RUNTIME_COUNT(n) is 1 there; in C++ it is n.
+inline thread_local int pbr_num_dir = 0, pbr_num_point = 0, pbr_num_spot = 0;
+constexpr int pbr_pp_one = 1;
+#define PBR_RUNTIME_COUNT(n) ((n) + 1 - pbr_pp_one)
 
-float3 direct_light(const oracle_pass& ps, const oracle_light* lights, const ref_d4::Material& mat, float3 pos,
-                    float3 N, float3 V) {
-    float3 r;
-    if (try_permutation<4, 0, 0, ref_d4::Light>(ps, lights, mat, pos, N, V, r, ref_d4::ComputeLighting)) return r;
-    {
-        ref_p1::Material m1 = {mat.DiffuseAlbedo, mat.Metallic, mat.FresnelR0, mat.Roughness, mat.Transmission,
-                               mat.Opacity, mat.Emissive, mat.Sheen, mat.ClearCoatThickness, mat.ClearCoatRoughness,
-                               mat.Anisotropy, mat.AnisotropyRotation};
-        if (try_permutation<0, 1, 0, ref_p1::Light>(ps, lights, m1, pos, N, V, r, ref_p1::ComputeLighting)) return r;
-        ref_p8::Material m8 = {mat.DiffuseAlbedo, mat.Metallic, mat.FresnelR0, mat.Roughness, mat.Transmission,
-                               mat.Opacity, mat.Emissive, mat.Sheen, mat.ClearCoatThickness, mat.ClearCoatRoughness,
-                               mat.Anisotropy, mat.AnisotropyRotation};
-        if (try_permutation<0, 8, 0, ref_p8::Light>(ps, lights, m8, pos, N, V, r, ref_p8::ComputeLighting)) return r;
-        ref_mix::Material mm = {mat.DiffuseAlbedo, mat.Metallic, mat.FresnelR0, mat.Roughness, mat.Transmission,
-                                mat.Opacity, mat.Emissive, mat.Sheen, mat.ClearCoatThickness, mat.ClearCoatRoughness,
-                                mat.Anisotropy, mat.AnisotropyRotation};
-        if (try_permutation<4, 8, 4, ref_mix::Light>(ps, lights, mm, pos, N, V, r, ref_mix::ComputeLighting)) return r;
-    }
-    // Any other count: ComputeLighting's three loops (LightingUtil.hlsl:176-199) over the reference's
-    // per-light functions, same order, same `result +=`, same shadowFactor multiply on directional lights.
-    float3 result = 0.0f;
-    float3 shadowFactor = 1.0f;
-    int i = 0;
-    ref_d4::Light L;
-    for (i = 0; i < ps.n_dir; i++) {
-        to_ref_light(lights[i], L);
-        result += shadowFactor * ref_d4::ComputeDirectionalLight(L, mat, N, V);
-    }
-    for (i = ps.n_dir; i < ps.n_dir + ps.n_point; i++) {
-        to_ref_light(lights[i], L);
-        result += ref_d4::ComputePointLight(L, mat, pos, N, V);
-    }
-    for (i = ps.n_dir + ps.n_point; i < ps.n_dir + ps.n_point + ps.n_spot; i++) {
-        to_ref_light(lights[i], L);
-        result += ref_d4::ComputeSpotLight(L, mat, pos, N, V);
-    }
-    return result;
-}
+#define DIFFUSE_TEXTURE 1
+#define METALLIC_TEXTURE 1
+#define ROUGHNESS_TEXTURE 1
+#define NORMAL_TEXTURE 1
+#define ALPHA_TEST 0
+#define DISPLACEMENT_TEXTURE 0
 
-}  // namespace
+// Default.hlsl as shipped (constant ambient, Default.hlsl:150).
+#define NUM_DIR_LIGHTS PBR_RUNTIME_COUNT(pbr_num_dir)
+#define NUM_POINT_LIGHTS PBR_RUNTIME_COUNT(pbr_num_point)
+#define NUM_SPOT_LIGHTS PBR_RUNTIME_COUNT(pbr_num_spot)
+#define SPECULAR_TEXTURE 0
+namespace ps_const {
+#include "Default.hlsl"
+#include "ps_binding.inc"
+}  // namespace ps_const
+namespace ps_ibl {
+#include "Default_ibl.hlsl"
+#include "ps_binding.inc"
+}  // namespace ps_ibl
+#undef SPECULAR_TEXTURE
+#define SPECULAR_TEXTURE 1
+namespace ps_const_f0map {
+#include "Default.hlsl"
+#include "ps_binding.inc"
+}  // namespace ps_const_f0map
+namespace ps_ibl_f0map {
+#include "Default_ibl.hlsl"
+#include "ps_binding.inc"
+}  // namespace ps_ibl_f0map
+#undef SPECULAR_TEXTURE
+#undef NUM_DIR_LIGHTS
+#undef NUM_POINT_LIGHTS
+#undef NUM_SPOT_LIGHTS
+
+// The shipped permutation: Core.hlsl:1-12 supplies its own 4 / 0 / 0 counts.
+#define SPECULAR_TEXTURE 0
+namespace ps_shipped {
+#include "Default.hlsl"
+#include "ps_binding.inc"
+constexpr int kDir = NUM_DIR_LIGHTS, kPoint = NUM_POINT_LIGHTS, kSpot = NUM_SPOT_LIGHTS;
+}  // namespace ps_shipped
+#undef NUM_DIR_LIGHTS
+#undef NUM_POINT_LIGHTS
+#undef NUM_SPOT_LIGHTS
+
+// Skybox.hlsl (its PS reads g_SkyArray[0] only; no light loop runs).
+namespace sky {
+#include "Skybox.hlsl"
+}  // namespace sky
+#undef NUM_DIR_LIGHTS
+#undef NUM_POINT_LIGHTS
+#undef NUM_SPOT_LIGHTS
+#undef SPECULAR_TEXTURE
+
+}  // namespace hlsl
+
+using namespace hlsl;
 
 namespace {
 
-// PS (Default.hlsl:47-161) for one G-buffer pixel.
-float4 ps_pixel(const float* const* planes, int64_t i, const oracle_pass& ps, const oracle_light* lights,
-                const Texture2D& env) {
+enum Variant { kShipped, kConst, kIbl, kConstF0, kIblF0 };
+
+Variant pick(const oracle_pass& ps) {
+    const bool ibl = ps.ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE;
+    if (ps.use_f0_plane) return ibl ? kIblF0 : kConstF0;
+    if (ibl) return kIbl;
+    if (ps.n_dir == ps_shipped::kDir && ps.n_point == ps_shipped::kPoint && ps.n_spot == ps_shipped::kSpot)
+        return kShipped;
+    return kConst;
+}
+
+void bind(Variant v, const oracle_pass& ps, const oracle_light* lights, const Texture2D& env) {
+    pbr_num_dir = ps.n_dir;
+    pbr_num_point = ps.n_point;
+    pbr_num_spot = ps.n_spot;
+    switch (v) {
+        case kShipped: ps_shipped::pbr_bind_pass(ps, lights, env); break;
+        case kConst: ps_const::pbr_bind_pass(ps, lights, env); break;
+        case kIbl: ps_ibl::pbr_bind_pass(ps, lights, env); break;
+        case kConstF0: ps_const_f0map::pbr_bind_pass(ps, lights, env); break;
+        case kIblF0: ps_ibl_f0map::pbr_bind_pass(ps, lights, env); break;
+    }
+    if (ps.apply_ao && v != kConst) ps_const::pbr_bind_pass(ps, lights, env);  // ps_pixel_ao_extension's
+}
+
+// Extension, not in the reference (the reference never reads its AO map): the same PS with
+// the ambient term multiplied by the G-buffer AO. Restated line by line from Default.hlsl:47-161 on the
+// compiled reference functions (ps_const / ps_ibl namespaces: ComputeLighting, FresnelSchlick,
+// WorldToSkyUV, lerp); pbr_bind_pass must have run for the pass.
+float4 ps_pixel_ao_extension(const float* const* planes, int64_t i, const oracle_pass& ps, const Texture2D& env) {
     float3 PosW(planes[ORACLE_PX][i], planes[ORACLE_PY][i], planes[ORACLE_PZ][i]);
     float3 N(planes[ORACLE_NX][i], planes[ORACLE_NY][i], planes[ORACLE_NZ][i]);
-    float3 g_CameraPosW(ps.eye[0], ps.eye[1], ps.eye[2]);
-    // Default.hlsl:53
-    float3 V = normalize(g_CameraPosW - PosW);
-    float3 diffuseAlbedo(planes[ORACLE_AR][i], planes[ORACLE_AG][i], planes[ORACLE_AB][i]);
-    float metallic = planes[ORACLE_METAL][i];
-    float roughness = planes[ORACLE_ROUGH][i];
+    float3 V = normalize(ps_const::cbPass::g_CameraPosW - PosW);                        // :53
+    float3 diffuseAlbedo(planes[ORACLE_AR][i], planes[ORACLE_AG][i], planes[ORACLE_AB][i]);  // :80
+    float metallic = planes[ORACLE_METAL][i];                                                 // :86
+    float roughness = planes[ORACLE_ROUGH][i];                                                // :99
     float3 F0;
-    if (ps.use_f0_plane) {  // Default.hlsl:92
-        F0 = float3(planes[ORACLE_F0R][i], planes[ORACLE_F0G][i], planes[ORACLE_F0B][i]);
-    } else {  // Default.hlsl:94-95
-        F0 = float3(ps.fresnel_r0[0], ps.fresnel_r0[1], ps.fresnel_r0[2]);
-        F0 = lerp(F0, diffuseAlbedo, metallic);
+    if (ps.use_f0_plane) {
+        F0 = float3(planes[ORACLE_F0R][i], planes[ORACLE_F0G][i], planes[ORACLE_F0B][i]);  // :92
+    } else {
+        F0 = float3(ps.fresnel_r0[0], ps.fresnel_r0[1], ps.fresnel_r0[2]);                  // :94
+        F0 = lerp(F0, diffuseAlbedo, metallic);                                             // :95
     }
-    // Default.hlsl:121-133 (only the first four members are read by the BRDF)
-    ref_d4::Material mat = {diffuseAlbedo, metallic, F0, roughness, float3(1.0f), ps.opacity,
-                            float3(0.0f), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    // Default.hlsl:135-137
-    float3 directLight = direct_light(ps, lights, mat, PosW, N, V);
+    ps_const::Material mat = {diffuseAlbedo, metallic, F0, roughness, float3(1.0f), ps.opacity,
+                              float3(0.0f), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};                  // :121-133
+    float3 shadowFactor = 1.0f;
+    float3 directLight = ps_const::ComputeLighting(ps_const::cbPass::g_Lights, mat, PosW, N, V, shadowFactor);
     float3 ambient;
-    if (ps.ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE) {
-        // Default.hlsl:141-146 (the commented-out IBL block)
-        float3 kS = ref_d4::FresnelSchlick(N, V, F0);
+    if (ps.ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE) {  // :141-146
+        float3 kS = ps_const::FresnelSchlick(N, V, F0);
         float3 kD = 1.0f - kS;
         kD *= (1.0f - metallic);
-        float3 irradiance = env.Sample(ref_d4::WorldToSkyUV(N));
+        float3 irradiance = env.Sample(SamplerState{}, ps_const::WorldToSkyUV(N)).rgb();
         float3 diffuse = irradiance * diffuseAlbedo;
         ambient = (kD * diffuse);
     } else {
-        // Default.hlsl:150  g_AmbientLight * diffuseAlbedo
-        float4 g_AmbientLight{ps.ambient[0], ps.ambient[1], ps.ambient[2], 1.0f};
-        ambient = g_AmbientLight.rgb() * diffuseAlbedo;
+        ambient = ps_const::cbPass::g_AmbientLight * diffuseAlbedo;  // :150
     }
-    if (ps.apply_ao) ambient = ambient * planes[ORACLE_AO][i];  // extension, off in the reference
+    ambient = ambient * planes[ORACLE_AO][i];  // the extension
     float3 litColor = ambient + directLight;
-    // Default.hlsl:153, 155
-    litColor = litColor / (litColor + float3(1.0f, 1.0f, 1.0f));
-    litColor = pow(litColor, (1.0f / 2.2f));
-    return float4{litColor.x, litColor.y, litColor.z, ps.opacity};  // Default.hlsl:160
+    litColor = litColor / (litColor + float3(1.0f, 1.0f, 1.0f));  // :153
+    litColor = pow(litColor, (1.0f / 2.2f));                      // :155
+    return float4(litColor, ps.opacity);                          // :160
 }
 
-// Skybox.hlsl:41-49 (PS) for one background pixel; PosW = the G-buffer normal planes.
-float4 sky_pixel(const float* const* planes, int64_t i, const Texture2D& sky) {
-    float3 PosW(planes[ORACLE_NX][i], planes[ORACLE_NY][i], planes[ORACLE_NZ][i]);
-    float3 sampleCoord = normalize(PosW);
-    sampleCoord = ref_d4::WorldToSkyUV(sampleCoord);
-    float3 skyColor = sky.Sample(sampleCoord);
-    skyColor = skyColor / (skyColor + float3(1.0f, 1.0f, 1.0f));
-    skyColor = pow(skyColor, (1.0f / 2.2f));
-    return float4{skyColor.x, skyColor.y, skyColor.z, 1.0f};
+float4 shade_pixel(Variant v, const float* const* planes, int64_t i, const oracle_pass& ps, const Texture2D& env) {
+    if (ps.apply_ao) return ps_pixel_ao_extension(planes, i, ps, env);
+    switch (v) {
+        case kShipped: return ps_shipped::pbr_shade_pixel(planes, i);
+        case kConst: return ps_const::pbr_shade_pixel(planes, i);
+        case kIbl: return ps_ibl::pbr_shade_pixel(planes, i);
+        case kConstF0: return ps_const_f0map::pbr_shade_pixel(planes, i);
+        case kIblF0: return ps_ibl_f0map::pbr_shade_pixel(planes, i);
+    }
+    return float4();
+}
+
+// Skybox.hlsl PS for one background pixel; the dome's interpolated local position (pin.PosW) is the
+// G-buffer normal planes.
+float4 sky_pixel(const float* const* planes, int64_t i) {
+    sky::VertexOut pin;
+    pin.PosW = float3(planes[ORACLE_NX][i], planes[ORACLE_NY][i], planes[ORACLE_NZ][i]);
+    return sky::PS(pin);
 }
 
 uint8_t unorm8(float c) {  // D3D FLOAT -> UNORM (the R8G8B8A8_UNORM back buffer, d3dApp.h:124)
@@ -222,21 +245,30 @@ uint8_t unorm8(float c) {  // D3D FLOAT -> UNORM (the R8G8B8A8_UNORM back buffer
     return (uint8_t)(c * 255.0f + 0.5f);
 }
 
+bool counts_ok(const oracle_pass& ps) {
+    return ps.n_dir >= 0 && ps.n_point >= 0 && ps.n_spot >= 0 &&
+           (int64_t)ps.n_dir + ps.n_point + ps.n_spot <= PBR_ORACLE_MAX_LIGHTS;
+}
+
 }  // namespace
 
 extern "C" int ref_shade_frame(int width, int height, int64_t stride, const float* const* planes,
                                const oracle_pass* pass, const oracle_light* lights, const oracle_frame* frame,
                                void* out, int64_t out_stride, int /*n_threads*/) {
-    if (!planes || !pass || !frame || !out || width < 0 || height < 0) return -1;
+    if (!planes || !pass || !frame || !out || width < 0 || height < 0 || !counts_ok(*pass)) return -1;
     if (pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE && !frame->env_rgba) return -1;
     if (frame->coverage && !frame->sky_rgba) return -1;
-    Texture2D env{nullptr, frame->env_w, frame->env_h, frame->env_rgba};
-    Texture2D sky{nullptr, frame->sky_w, frame->sky_h, frame->sky_rgba};
+    Texture2D env, skytex;
+    env.ftexels = frame->env_rgba, env.w = frame->env_w, env.h = frame->env_h;
+    skytex.ftexels = frame->sky_rgba, skytex.w = frame->sky_w, skytex.h = frame->sky_h;
+    const Variant v = pick(*pass);
+    bind(v, *pass, lights, env);
+    sky::g_SkyArray[0] = skytex;  // Core.hlsl:16, PBRApp.cpp:1205-1210
     for (int y = 0; y < height; ++y) {
         for (int x = 0; x < width; ++x) {
             const int64_t i = (int64_t)y * stride + x;
             const bool background = frame->coverage && frame->coverage[(int64_t)y * frame->coverage_stride + x] == 0;
-            const float4 c = background ? sky_pixel(planes, i, sky) : ps_pixel(planes, i, *pass, lights, env);
+            const float4 c = background ? sky_pixel(planes, i) : shade_pixel(v, planes, i, *pass, env);
             const int64_t off = ((int64_t)y * out_stride + x) * 4;
             if (frame->format == ORACLE_OUTPUT_RGBA8) {
                 uint8_t* o = static_cast<uint8_t*>(out) + off;
@@ -253,12 +285,15 @@ extern "C" int ref_shade_frame(int width, int height, int64_t stride, const floa
 extern "C" int ref_shade(int width, int height, int64_t stride, const float* const* planes, const oracle_pass* pass,
                          const oracle_light* lights, const uint16_t* env_rgba16, int env_w, int env_h, float* out,
                          int64_t out_stride, int /*n_threads*/) {
-    if (!planes || !pass || !out || width < 0 || height < 0) return -1;
+    if (!planes || !pass || !out || width < 0 || height < 0 || !counts_ok(*pass)) return -1;
     if (pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE && !env_rgba16) return -1;
-    Texture2D env{env_rgba16, env_w, env_h};
+    Texture2D env;
+    env.texels = env_rgba16, env.w = env_w, env.h = env_h;
+    const Variant v = pick(*pass);
+    bind(v, *pass, lights, env);
     for (int y = 0; y < height; ++y) {
         for (int x = 0; x < width; ++x) {
-            const float4 c = ps_pixel(planes, (int64_t)y * stride + x, *pass, lights, env);
+            const float4 c = shade_pixel(v, planes, (int64_t)y * stride + x, *pass, env);
             float* o = out + ((int64_t)y * out_stride + x) * 4;
             o[0] = c.x; o[1] = c.y; o[2] = c.z; o[3] = c.w;
         }

@@ -1,8 +1,11 @@
 """Generate the golden vectors in tests/golden/*.npz (run in the build container only).
 
 Each fixture holds a small SoA G-buffer, a light list, the pass constants and the RGBA output of
-``oracle/_ref/libpbr_ref.so`` -- the reference's own ``Source/Shaders/LightingUtil.hlsl`` compiled as
-C++ (oracle/ref_harness.cpp) -- for the same inputs. The fixtures pin ``oracle/pbr_oracle.c``
+``oracle/_ref/libpbr_ref.so`` -- the reference's own pixel-shader text (``Default.hlsl``'s PS with
+``Core.hlsl`` and ``LightingUtil.hlsl``; ``Skybox.hlsl``'s PS for background pixels) compiled as C++
+(oracle/strip_hlsl.py, oracle/ref_harness.cpp) -- for the same inputs. The fixtures were first made by an
+earlier harness that compiled only LightingUtil.hlsl and restated the PS composition; the compiled PS
+reproduces every one of them bit for bit (tests/test_oracle_golden.py::test_reference_build_reproduces_*). The fixtures pin ``oracle/pbr_oracle.c``
 (tests/test_oracle_golden.py) on machines where /root/reference is absent (the GPU box).
 
     make -C oracle all ref && python tests/golden/gen_golden.py            # everything

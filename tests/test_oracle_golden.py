@@ -1,5 +1,6 @@
-"""The oracle (oracle/pbr_oracle.c) against the golden vectors made by the reference's own
-LightingUtil.hlsl compiled as C++ (oracle/_ref, tests/golden/gen_golden.py).
+"""The oracle (oracle/pbr_oracle.c) against the golden vectors made by the reference's own shader text
+compiled as C++ (oracle/_ref: Default.hlsl's PS with Core.hlsl and LightingUtil.hlsl, Skybox.hlsl's PS;
+oracle/strip_hlsl.py, tests/golden/gen_golden.py).
 
 Bar: bit equality (NaN == NaN), since both run the same fp32 operations in the same order on the
 same libm. When /root/reference is present the reference build is also re-run here on fresh random
@@ -118,3 +119,70 @@ def test_frame_oracle_matches_reference_build_random(fmt, env_map):
     a = O.shade_frame(list(p), ps, lights, env_map, sky, cov, fmt, n_threads=2)
     b = O.shade_frame_ref(list(p), ps, lights, env_map, sky, cov, fmt)
     assert (np.array_equal(a, b) if fmt == O.OUTPUT_RGBA8 else O.bit_equal(a, b).all())
+
+
+# ---- the reference build itself: the compiled PS / Skybox PS text (oracle/strip_hlsl.py) ------------------
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref needs /root/reference (build container only)")
+@pytest.mark.parametrize("name", golden_names())
+def test_reference_build_reproduces_golden(name, env_map):
+    """oracle/_ref -- Default.hlsl's PS (or its revived IBL block) compiled from the reference text --
+    reproduces every committed golden bit for bit."""
+    planes, lights, meta, expected = load_golden(name)
+    ps = oracle_pass_from_meta(meta)
+    got = O.shade_ref(list(planes), ps, lights, env_map if meta["env"] else None)
+    assert O.bit_equal(got, expected).all()
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref needs /root/reference (build container only)")
+@pytest.mark.parametrize("name", frame_golden_names())
+def test_reference_build_reproduces_frame_golden(name, env_map):
+    g = load_frame_golden(name, env_map)
+    ps = oracle_pass_from_meta(g["meta"])
+    got = O.shade_frame_ref(list(g["planes"]), ps, g["lights"], g["env"], g["sky"], g["coverage"], g["meta"]["format"])
+    assert (np.array_equal(got, g["expected"]) if g["meta"]["format"] == O.OUTPUT_RGBA8
+            else O.bit_equal(got, g["expected"]).all())
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref needs /root/reference (build container only)")
+def test_reference_build_shipped_permutation_equals_runtime_counts():
+    """Core.hlsl's own 4/0/0 permutation (compile-time counts) and the runtime-count build agree: the
+    harness runs the shipped one for a 4-directional-light pass, the runtime one for 4 dir + 0-strength
+    point light appended (which adds +0 to every channel, ComputeLighting order)."""
+    planes, lights, meta, expected = load_golden("reference_scene_red_spheres")
+    ps = oracle_pass_from_meta(meta)
+    assert (ps.n_dir, ps.n_point, ps.n_spot) == (4, 0, 0)
+    shipped = O.shade_ref(list(planes), ps, lights)
+    extra = np.concatenate([lights, np.zeros((1, 12), np.float32)])
+    extra[-1, 8:11] = 1e6  # beyond the 100-unit range: the reference returns exactly 0 (LightingUtil.hlsl:131)
+    ps2 = O.OraclePass(**{**ps.__dict__, "n_point": 1})
+    runtime = O.shade_ref(list(planes), ps2, extra)
+    assert O.bit_equal(shipped, runtime).all() and O.bit_equal(shipped, expected).all()
+
+
+def test_strip_hlsl_rules_are_syntax_only(tmp_path):
+    """The transform on a miniature of the reference's syntax: every rule fires, and a mismatched count
+    fails loudly (so a changed reference text cannot pass silently)."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location("strip_hlsl", os.path.join(O.HERE, "strip_hlsl.py"))
+    sh = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sh)
+    src = ("Texture2D g_Tex[2] : register(t0);\nSamplerState g_S : register(s0);\n"
+           "cbuffer cbPass : register(b1)\n{\n    float3 g_Eye;\n    Light g_Lights[MAX_LIGHTS];\n};\n"
+           "struct VertexOut { float4 PosH : SV_POSITION; float3 PosW : POSITION; };\n"
+           "float4 PS(VertexOut pin) : SV_Target\n{\n    VertexOut v = (VertexOut)0.0f;\n"
+           "    return float4(g_Tex[0].Sample(g_S, pin.PosW.xy).rgb, 1.0f);\n}\n")
+    sh.EXPECT["mini"] = dict(register=3, cbuffer=1, resources=2, semantics=2, sv_target=1, swizzles=2, zero_cast=1,
+                             capacity=1)
+    out = sh.common(src, "mini")
+    assert "register" not in out and ": SV_Target" not in out and "cbuffer" not in out
+    assert "inline namespace cbPass {" in out and "PBR_HLSL_GLOBAL float3 g_Eye;" in out
+    assert "PBR_HLSL_GLOBAL Light g_Lights[PBR_ORACLE_MAX_LIGHTS];" in out
+    assert "PBR_HLSL_GLOBAL Texture2D g_Tex[2];" in out and "PBR_HLSL_GLOBAL SamplerState g_S;" in out
+    assert ".xy()" in out and ".rgb()" in out and "VertexOut{}" in out
+    # a rule that fires a different number of times than the reference text implies is an error
+    sh.EXPECT["mini"]["swizzles"] = 3
+    with pytest.raises(SystemExit):
+        sh.common(src, "mini")
