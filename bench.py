@@ -90,48 +90,91 @@ def load_pmc(workload: str):
         return None, None
 
 
-def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int, kind: str = "auto"):
-    """Time the reference CPU shader path on every k-th row of the frame (rank 0, N = 1) and check parity
-    there. kind "reference": the reference's own pixel shader (Default.hlsl PS + Core.hlsl + LightingUtil.hlsl)
-    compiled as C++ (oracle/_ref, built in
-    the build container; nothing under /root/reference is read at run time), one row band per host thread;
-    kind "port": the C restatement oracle/pbr_oracle.c (pthreads). "auto" takes the reference build when
-    it is present. Both are test infrastructure, used here only as the CPU baseline and the checker."""
+def host_cpu_budget() -> dict:
+    """The host cores this process may use: the affinity mask, the whole machine (os.cpu_count), and the
+    cgroup CPU quota (cpu.max, in CPUs) when one caps the container below its affinity. `used` = the
+    threads the CPU baseline runs: the affinity count, capped by the quota (threads beyond the quota
+    would only be throttled)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    used = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"affinity": aff, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota, "used": used}
+
+
+def oracle_pass_of(pc):
+    from oracle import oracle as O  # test infrastructure: the checker / CPU baseline only
+
+    return O.OraclePass(eye=tuple(pc.eye_pos_w), ambient=tuple(pc.ambient_light), fresnel_r0=tuple(pc.fresnel_r0),
+                        opacity=pc.opacity, n_dir=pc.num_dir_lights, n_point=pc.num_point_lights,
+                        n_spot=pc.num_spot_lights, ambient_mode=pc.ambient_mode,
+                        use_f0_plane=bool(pc.flags & N.PBR_FLAG_F0_PLANE),
+                        apply_ao=bool(pc.flags & N.PBR_FLAG_APPLY_AO))
+
+
+def cpu_shade(planes, pc, env, threads: int, use_ref: bool, rgba8: bool):
+    """The CPU shader path over (15, rows, W) host planes in the bench's output format: the reference's own
+    shader text built for the host (oracle/_ref, one row band per thread; ctypes releases the GIL) or the C
+    restatement (oracle/pbr_oracle.c, pthreads)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O  # test infrastructure: the checker / CPU baseline only
 
+    ops, lights = oracle_pass_of(pc), pc.light_array()
+    fmt = O.OUTPUT_RGBA8 if rgba8 else O.OUTPUT_RGBA32F
+    if not use_ref:
+        return O.shade_frame(list(planes), ops, lights, env, None, None, fmt, n_threads=threads)
+    edges = np.linspace(0, planes.shape[1], threads + 1).astype(int)
+    bands = [np.ascontiguousarray(planes[:, a:b]) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+    with ThreadPoolExecutor(len(bands)) as ex:
+        parts = ex.map(lambda b: O.shade_frame_ref(list(b), ops, lights, env, None, None, fmt), bands)
+        return np.concatenate(list(parts), axis=0)
+
+
+def parity_of(got, ref, rgba8: bool) -> dict:
+    """fp32: max relative error per channel (NaN == NaN) and the bit-identical fraction; RGBA8: the largest
+    code difference and the identical fraction (a 1e-5 relative difference can move a code by one where
+    c * 255 + 0.5 sits on an integer)."""
+    from oracle import oracle as O  # test infrastructure: the checker only
+
+    if rgba8:
+        d = np.abs(got.astype(np.int32) - ref.astype(np.int32))
+        return {"parity_max_code_diff": int(d.max()) if d.size else 0,
+                "parity_bit_exact_frac": round(float((d == 0).mean()) if d.size else 1.0, 6)}
+    return {"parity_max_rel": float(O.rel_err(got, ref).max()) if got.size else 0.0,
+            "parity_bit_exact_frac": round(float(O.bit_equal(got, ref).mean()) if got.size else 1.0, 6)}
+
+
+def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int, kind: str = "auto", rgba8: bool = False):
+    """Time the reference CPU shader path on every k-th row of the frame (rank 0, N = 1) and check parity
+    there. kind "reference": the reference's own pixel shader (Default.hlsl PS + Core.hlsl + LightingUtil.hlsl)
+    compiled as C++ (oracle/_ref, built in the build container; nothing under /root/reference is read at run
+    time), one row band per host thread; kind "port": the C restatement oracle/pbr_oracle.c (pthreads). "auto"
+    takes the reference build when it is present. Both are test infrastructure, used here only as the CPU
+    baseline and the checker. Threads: every core of the affinity mask (capped by a cgroup quota)."""
+    from oracle import oracle as O  # test infrastructure: the checker / CPU baseline only
+
     use_ref = kind == "reference" or (kind == "auto" and O.ref_available())
-    n_threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    budget = host_cpu_budget()
+    n_threads = budget["used"]
     step = max(1, cfg.height // budget_rows) if budget_rows > 0 else 1
     sample = np.ascontiguousarray(planes_host[:, ::step])
-    ops = O.OraclePass(eye=tuple(pc.eye_pos_w), ambient=tuple(pc.ambient_light), fresnel_r0=tuple(pc.fresnel_r0),
-                       opacity=pc.opacity, n_dir=pc.num_dir_lights, n_point=pc.num_point_lights,
-                       n_spot=pc.num_spot_lights, ambient_mode=pc.ambient_mode,
-                       use_f0_plane=bool(pc.flags & N.PBR_FLAG_F0_PLANE),
-                       apply_ao=bool(pc.flags & N.PBR_FLAG_APPLY_AO))
-    lights = pc.light_array()
-
-    def run(planes, threads):
-        if not use_ref:
-            return O.shade(list(planes), ops, lights, env, n_threads=threads)
-        edges = np.linspace(0, planes.shape[1], threads + 1).astype(int)
-        bands = [np.ascontiguousarray(planes[:, a:b]) for a, b in zip(edges[:-1], edges[1:]) if b > a]
-        with ThreadPoolExecutor(len(bands)) as ex:  # ctypes releases the GIL inside each call
-            return np.concatenate(list(ex.map(lambda b: O.shade_ref(list(b), ops, lights, env), bands)), axis=0)
-
     t0 = time.perf_counter()
-    ref = run(sample, n_threads)
+    ref = cpu_shade(sample, pc, env, n_threads, use_ref, rgba8)
     dt = time.perf_counter() - t0
     px = sample.shape[1] * sample.shape[2]
     # single-thread rate on the first 8 sampled rows (SURVEY 8(d): single-thread and all-core)
     one = np.ascontiguousarray(sample[:, :8])
     t1 = time.perf_counter()
-    run(one, 1)
+    cpu_shade(one, pc, env, 1, use_ref, rgba8)
     st = one.shape[1] * one.shape[2] / (time.perf_counter() - t1) / 1e6
-    got = gpu_frame[::step]
-    err = O.rel_err(got, ref)
-    exact = float(O.bit_equal(got, ref).mean())
+    parity = parity_of(gpu_frame[::step], ref, rgba8)
     model = None
     try:
         for line in open("/proc/cpuinfo"):
@@ -140,17 +183,33 @@ def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int, kind: s
                 break
     except OSError:
         pass
-    what = ("oracle/_ref/libpbr_ref.so: the reference's Default.hlsl PS (+ Core/LightingUtil.hlsl) compiled as C++ (g++ -O2 "
-            f"-ffp-contract=off), {n_threads} host threads over row bands" if use_ref else
+    what = ("oracle/_ref/libpbr_ref.so: the reference's Default.hlsl PS (+ Core/LightingUtil.hlsl) compiled as "
+            f"C++ (g++ -O2 -ffp-contract=off), {n_threads} host threads over row bands" if use_ref else
             f"oracle/pbr_oracle.c, -O2 -ffp-contract=off, {n_threads} pthreads")
     return {
         "value": round(px / dt / 1e6, 4), "unit": "Mpix/s", "cores": n_threads,
+        "host_cpus": budget,
         "kind": "reference" if use_ref else "port",
         "cpu_model": model,
         "single_thread_value": round(st, 4),
         "sample": (f"every {step}th row of" if step > 1 else "all rows of") +
                   f" the same {cfg.width}x{cfg.height} frame ({px} px, {dt:.2f} s wall), {what}",
-    }, float(err.max()), exact, (step, ref)
+    }, parity, (step, ref)
+
+
+def gathered_parity(cfg, pc, env, frame: np.ndarray, world: int, rows_per_band: int, rgba8: bool) -> dict:
+    """Rank 0 at N > 1: the assembled frame against the CPU oracle on `rows_per_band` rows of every rank's
+    band (spread over the band; the G-buffer rows are refilled on the host, the fill being a function of
+    the global pixel). Untimed."""
+    from oracle import oracle as O  # test infrastructure: the checker only
+
+    rows = []
+    for r in range(world):
+        b = D.band_rows(cfg.height, world, r)
+        rows += sorted({b.row_begin + (k * b.rows) // rows_per_band for k in range(rows_per_band)} if b.rows else [])
+    planes = np.concatenate([S.fill_gbuffer_host(cfg, y, y + 1)[0] for y in rows], axis=1)
+    ref = cpu_shade(planes, pc, env, host_cpu_budget()["used"], O.ref_available(), rgba8)
+    return {"rows_checked": len(rows), **parity_of(frame[rows], ref, rgba8)}
 
 
 def time_exact_mode(ctx, pc, gb, out, stream, args, fmt, rgba8, px):
@@ -196,16 +255,19 @@ def main():
     ap.add_argument("--config", type=int, default=0, help="BASELINE config id (default 3 at N=1, 5 at N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rows-per-rank", type=int, default=1024,
-                    help="config 5 band height per rank at N > 1 (1024 = the BASELINE geometry; smaller only "
-                         "for rehearsing the multi-rank path)")
+                    help="config 5 band height per rank (1024 = the BASELINE geometry: 8192x8192 at N = 8; "
+                         "smaller only for rehearsing the multi-rank path). The same band at every N, N = 1 "
+                         "included, so per-GPU work is identical across the scaling curve")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (the benchmark); gloo = host-staged gather, for exercising the "
                          "multi-rank path on one GPU")
     ap.add_argument("--output", default="auto", choices=["auto", "rgba32f", "rgba8"],
-                    help="output format: fp32 RGBA or the reference's R8G8B8A8_UNORM back buffer (fused conversion, "
-                         "4x smaller multi-GPU gather). auto = rgba32f at N = 1 (the frame the parity check reads), "
-                         "rgba8 at N > 1 (the presented frame rank 0 assembles; an fp32 band is 134 MB per xGMI "
-                         "link per frame, longer than the band's shading, DESIGN.md section 7)")
+                    help="output format: fp32 RGBA or the reference's R8G8B8A8_UNORM back buffer (fused conversion). "
+                         "auto = rgba32f for the single-GPU configs 1-4 (the frame the parity check reads), rgba8 "
+                         "for config 5 at every N (the presented frame rank 0 assembles; an fp32 band is 134 MB "
+                         "per xGMI link per frame, longer than the band's shading, DESIGN.md section 7). "
+                         "--output rgba32f with config 5 gathers fp32 and checks the assembled frame against the "
+                         "oracle")
     ap.add_argument("--mode", default="faithful", choices=["exact", "faithful"],
                     help="faithful (default) = PBR_FLAG_FAITHFUL: hardware reciprocals (<= 1 ulp; D3D allows 2.5 ulp "
                          "for fp32 division) in the well-conditioned BRDF divisions, exact GGX/Fresnel chain, within "
@@ -218,7 +280,9 @@ def main():
                     help="CPU baseline: the reference's own shader source compiled for the host (oracle/_ref) or the "
                          "C restatement (oracle/pbr_oracle.c); auto = the reference build when present")
     ap.add_argument("--cpu-rows", type=int, default=0,
-                    help="rows in the CPU-baseline sample (0 = the whole frame: ~1.5 s on 16 host threads)")
+                    help="rows in the CPU-baseline sample (0 = the whole frame or band)")
+    ap.add_argument("--parity-rows", type=int, default=8,
+                    help="N > 1: rows per band of the assembled frame checked against the oracle (0 = none)")
     args = ap.parse_args()
 
     if not torch.cuda.is_available():
@@ -228,25 +292,28 @@ def main():
     if args.dist_backend == "nccl" and local_env >= n_dev:
         raise SystemExit(f"LOCAL_RANK {local_env} but only {n_dev} visible GPU(s): RCCL needs one GPU per rank")
     torch.cuda.set_device(local_env % n_dev)
-    rank, world, local = D.init_from_env(args.dist_backend)
+    # Under torch.distributed.run (WORLD_SIZE set) the process group is created at every world size, N = 1
+    # included, so the N = 1 line runs the same RCCL init, band gather and checksum collective as N = 8.
+    rank, world, local = D.init_from_env(args.dist_backend, always="WORLD_SIZE" in os.environ)
+    in_group = dist.is_initialized()
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
     device = torch.device("cuda", local % n_dev)
 
     cid = args.config or (3 if world == 1 else 5)
     cfg = S.CONFIGS[cid]
-    if world > 1 and cid == 5:
-        cfg = cfg.with_size(8192, args.rows_per_rank * world)  # 1024 rows per rank: 8192x8192 at N = 8
+    banded = cid == 5  # BASELINE config 5: row bands of --rows-per-rank rows, gathered to rank 0
+    if banded:
+        cfg = cfg.with_size(8192, args.rows_per_rank * world)
     band = D.band_rows(cfg.height, world, rank)
-    workload = f"{cfg.name}" + (f"_rows{cfg.height}" if cfg.height != S.CONFIGS[cid].height else "")
+    workload = f"{cfg.name}" + (f"_band{args.rows_per_rank}" if banded else "")
 
     t0 = time.perf_counter()
     pc = S.scene_pass(cfg)
     if args.mode == "faithful":
         pc.flags = int(pc.flags) | N.PBR_FLAG_FAITHFUL
     env = S.env_map() if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
-    import torch as _t
-    staging = _t.empty((N.NUM_PLANES, band.rows, cfg.width), dtype=_t.float32, pin_memory=True)
+    staging = torch.empty((N.NUM_PLANES, band.rows, cfg.width), dtype=torch.float32, pin_memory=True)
     S.fill_gbuffer_host(cfg, band.row_begin, band.row_end, out=staging.numpy())
     t_fill = time.perf_counter() - t0
     torch.cuda.synchronize()
@@ -262,26 +329,30 @@ def main():
     if env is not None:
         ctx.set_env_map(env)
     log(f"rank {rank}/{world}: {workload} rows [{band.row_begin},{band.row_end}) fill {t_fill:.2f}s "
-        f"upload {t_upload * 1e3:.1f} ms ({staging.numel() * 4 / t_upload / 1e9:.1f} GB/s H2D)")
+        f"upload {t_upload * 1e3:.1f} ms ({staging.numel() * 4 / t_upload / 1e9:.1f} GB/s H2D)"
+        + (f", process group {dist.get_backend()}" if in_group else ""))
 
-    output = args.output if args.output != "auto" else ("rgba32f" if world == 1 else "rgba8")
+    output = args.output if args.output != "auto" else ("rgba8" if banded else "rgba32f")
     rgba8 = output == "rgba8"
     out_dtype = torch.uint8 if rgba8 else torch.float32
     fmt = N.PBR_OUTPUT_RGBA8_UNORM if rgba8 else N.PBR_OUTPUT_RGBA32F
     outs = [torch.empty((band.rows_max, cfg.width, 4), dtype=out_dtype, device=device) for _ in range(2)]
-    gather = D.BandGather(band, cfg.width, device, dtype=out_dtype) if world > 1 else None
+    gather = D.BandGather(band, cfg.width, device, dtype=out_dtype) if banded else None
     stream = torch.cuda.current_stream(device)
     pending = [[], []]
+
+    def shade_into(o):
+        if rgba8:
+            ctx.shade_frame(gb, o, fmt=fmt, stream=stream)
+        else:
+            ctx.shade(gb, o, stream)
 
     def step(k: int, ev=None):
         slot = k % 2
         D.BandGather.wait(pending[slot])  # the gather that last read this slot (stream-side wait)
         if ev is not None:
             ev[0].record(stream)
-        if rgba8:
-            ctx.shade_frame(gb, outs[slot], fmt=fmt, stream=stream)
-        else:
-            ctx.shade(gb, outs[slot], stream)
+        shade_into(outs[slot])
         if ev is not None:
             ev[1].record(stream)
         if gather is not None:
@@ -291,10 +362,7 @@ def main():
     t_ramp = time.perf_counter()
     n_ramp = 0
     while args.ramp_ms > 0:
-        if rgba8:
-            ctx.shade_frame(gb, outs[0], fmt=fmt, stream=stream)
-        else:
-            ctx.shade(gb, outs[0], stream)
+        shade_into(outs[0])
         n_ramp += 1
         if n_ramp % 8 == 0:
             torch.cuda.synchronize()
@@ -307,7 +375,7 @@ def main():
         D.BandGather.wait(p)
     pending = [[], []]
     torch.cuda.synchronize()
-    if world > 1:
+    if in_group:
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -318,7 +386,7 @@ def main():
     for p in pending:
         D.BandGather.wait(p)
     torch.cuda.synchronize()
-    if world > 1:
+    if in_group:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
@@ -329,37 +397,47 @@ def main():
         kept, tiles = ctx.cull_stats(stream)  # of the last timed pass
         cull_note = {"lights_per_tile": round(kept / max(tiles, 1), 3), "tiles": tiles}
 
-    gather_ok = None
-    gather_ms = None
-    if world > 1:
+    coll_dev = device if args.dist_backend == "nccl" else torch.device("cpu")
+    gather_note = {}
+    if gather is not None:
         # The gather alone (no shading), timed the same way: the exchange cost the pipelined step hides.
         torch.cuda.synchronize()
-        dist.barrier()
+        if in_group:
+            dist.barrier()
         tg = time.perf_counter()
         for k in range(args.steps):
             D.BandGather.wait(gather.start(outs[k % 2]))
         torch.cuda.synchronize()
-        dist.barrier()
+        if in_group:
+            dist.barrier()
         gather_ms = (time.perf_counter() - tg) / args.steps * 1e3
-        # Property check of the assembled image: each rank's band checksum (int64 sum of the fp32 bit
-        # patterns, exact) must equal the checksum of the slot rank 0 received.
+        # Property check of the assembled image: each rank's band checksum (int64 sum of the 32-bit words,
+        # exact) must equal the checksum of the slot rank 0 received -- an all_gather on the device (RCCL).
         last = outs[(args.steps - 1) % 2][: band.rows].contiguous()
-        if rgba8:
-            last = last.view(torch.int32).squeeze(-1)
-        coll_dev = device if args.dist_backend == "nccl" else "cpu"
         mine = last.view(torch.int32).to(torch.int64).sum().reshape(1).to(coll_dev)
         sums = [torch.zeros(1, dtype=torch.int64, device=coll_dev) for _ in range(world)]
-        dist.all_gather(sums, mine)
+        if in_group:
+            dist.all_gather(sums, mine)
+        else:
+            sums = [mine]
+        gather_ok = None
         if rank == 0:
             got = [gather.frame[r, : D.band_rows(cfg.height, world, r).rows].contiguous().view(torch.int32)
                    .to(torch.int64).sum() for r in range(world)]
             gather_ok = all(int(g.item()) == int(s_.item()) for g, s_ in zip(got, sums))
+        gather_note = {
+            "gather": ("batched isend/irecv star to rank 0 (RCCL over xGMI), pipelined with the next frame"
+                       if in_group and args.dist_backend == "nccl" else
+                       "host-staged gloo gather (test mode)" if in_group else "rank 0's own band: device copy"),
+            "process_group": dist.get_backend() if in_group else None,
+            "gather_checksums_match": gather_ok, "gather_ms": round(gather_ms, 4),
+            "shade_ms": round(float(np.mean(kernel_ms)), 4)}
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=device if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
+    el = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+    if in_group and world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    total_px = cfg.width * cfg.height if world > 1 else cfg.width * band.rows
+    total_px = cfg.width * cfg.height
     value = total_px * args.steps / elapsed / 1e6
 
     if rank == 0:
@@ -368,18 +446,19 @@ def main():
         band_px = cfg.width * band.rows
         bpp = bytes_per_pixel(pc, 4 if rgba8 else 16)
         achieved = bpp * band_px / avg_kernel_s / 1e9
-        traffic, valu_busy = load_pmc(workload + ("_faithful" if args.mode == "faithful" else ""))
+        traffic, valu_busy = load_pmc(workload + ("_rgba8" if rgba8 and not banded else "")
+                                      + ("_faithful" if args.mode == "faithful" else ""))
         tile_px = 256 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 128  # culling unit: 32x8 / 64x2
         fpp = flops_per_pixel(pc, cull_note.get("lights_per_tile"), tile_px)
         tflops = fpp * band_px / avg_kernel_s / 1e12
         # At 64 lights the arithmetic intensity (fpp / bpp ~ 99 FLOP/B) is 5x the ridge point, so the
-        # compute roof bounds the kernel: FP32 at 157.3 TF (MI355X_MICROARCH.md: the FP32 vector rate,
-        # equal to the dense FP32 MFMA peak). HBM is reported beside it.
+        # FP32 vector (VALU) roof bounds the kernel: 157.3 TF (MI355X_MICROARCH.md). There is no matrix op
+        # on this path. HBM is reported beside it.
         compute_bound = fpp / bpp > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
         hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                "frac": round(achieved / HBM_PEAK_GBPS, 5)}
         roofline = {
-            "bound": "mfma" if compute_bound else "hbm",
+            "bound": "valu" if compute_bound else "hbm",
             "achieved": round(tflops, 3) if compute_bound else hbm["achieved"],
             "peak": FP32_PEAK_TFLOPS if compute_bound else HBM_PEAK_GBPS,
             "unit": "TFLOP/s" if compute_bound else "GB/s",
@@ -390,31 +469,27 @@ def main():
             "flop_per_px": fpp, "bytes_per_px": bpp, "px_per_launch": band_px,
             "hbm": hbm,
             "valu_issue_busy": valu_busy,
-            "note": ("compute roof = FP32 VALU (no matrix op on this path; the FP32 MFMA peak is the same "
-                     "157.3 TF); achieved counts the HLSL-level FLOPs (SURVEY 8(d)); valu_issue_busy = "
-                     "rocprofv3 SQ_ACTIVE_INST_VALU over kernel cycles, profiles/pmc_summary.json"),
+            "note": ("compute roof = the FP32 vector ALU (VALU, 157.3 TF packed; no matrix op on this path); "
+                     "achieved counts the HLSL-level FLOPs (SURVEY 8(d)); traffic = rocprofv3 FETCH_SIZE + "
+                     "WRITE_SIZE bytes per launch and valu_issue_busy = SQ_ACTIVE_INST_VALU over kernel cycles, "
+                     "both from profiles/pmc_summary.json"),
         }
         cpu = None
         parity = {}
         exact_leg = None
-        frame = outs[0][: band.rows].cpu().numpy() if world == 1 and not rgba8 else None
+        frame = outs[0][: band.rows].cpu().numpy() if world == 1 else None  # the timed mode's frame
+        exact_frame = None
         if world == 1 and args.mode == "faithful" and args.exact_leg:
-            exact_leg = time_exact_mode(ctx, pc, gb, outs[0], stream, args, fmt, rgba8, cfg.width * band.rows)
-        if frame is not None and not args.no_cpu_baseline:
-            cpu, max_rel, exact, (step, ref) = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows, args.cpu_kind)
-            parity = {"parity_max_rel": max_rel, "parity_bit_exact_frac": round(exact, 6)}
-            if exact_leg is not None:
-                from oracle import oracle as O  # test infrastructure: the checker only
-
-                got = outs[0][: band.rows].cpu().numpy()[::step]  # the exact-mode frame time_exact_mode left
-                exact_leg["parity_max_rel"] = float(O.rel_err(got, ref).max())
-                exact_leg["parity_bit_exact_frac"] = round(float(O.bit_equal(got, ref).mean()), 6)
-        gather_note = {}
-        if world > 1:
-            gather_note = {"gather": ("batched isend/irecv star to rank 0 (RCCL), pipelined with the next frame"
-                                      if args.dist_backend == "nccl" else "host-staged gloo gather (test mode)"),
-                           "gather_checksums_match": gather_ok, "gather_ms": round(gather_ms, 4),
-                           "shade_ms": round(avg_kernel_s * 1e3, 4)}
+            exact_leg = time_exact_mode(ctx, pc, gb, outs[0], stream, args, fmt, rgba8, band_px)
+            exact_frame = outs[0][: band.rows].cpu().numpy()
+        if world == 1 and not args.no_cpu_baseline:
+            cpu, parity, (step_, ref) = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows,
+                                                    args.cpu_kind, rgba8)
+            if exact_frame is not None:
+                exact_leg.update(parity_of(exact_frame[::step_], ref, rgba8))
+        elif world > 1 and gather is not None and args.parity_rows > 0:
+            parity = {"gathered_frame_parity": gathered_parity(cfg, pc, env, gather.assembled(cfg.height).cpu().numpy(),
+                                                               world, args.parity_rows, rgba8)}
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "clock_ramp": {"ms": round(ramp_ms, 1), "launches": n_ramp},
@@ -436,7 +511,7 @@ def main():
         }
         print(json.dumps(out), flush=True)
     ctx.close()
-    if world > 1:
+    if in_group:
         dist.destroy_process_group()
 
 

@@ -303,6 +303,10 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
         return PBR_ERR_INVALID_ARGUMENT;
     if (fr->format != PBR_OUTPUT_RGBA32F && fr->format != PBR_OUTPUT_RGBA8_UNORM) return PBR_ERR_INVALID_ARGUMENT;
     if (fr->coverage && fr->coverage_row_stride < gb->width) return PBR_ERR_INVALID_ARGUMENT;
+    // Everything below reads context state that pbr_set_pass / pbr_set_*_map write under the same
+    // mutex: the launch arguments are built (and the kernel queued) in one critical section, so a
+    // concurrent set_pass can never tear them.
+    std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ctx->pass_set) return PBR_ERR_NOT_READY;
     if (gb->width == 0 || gb->height == 0) return PBR_OK;  // empty frame: nothing is read or written
     if (!fr->out) return PBR_ERR_INVALID_ARGUMENT;
@@ -358,7 +362,6 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     hipError_t e;
     {
         const int64_t tiles = pbr::shade_tile_count(gb->width, gb->height, a.pixels_per_thread);
-        std::lock_guard<std::mutex> lk(ctx->mu);
         if (tiles > ctx->tile_kept_capacity) {
             // Growing: the old buffer may still be written by queued kernels on any stream.
             if (ctx->d_tile_kept) {

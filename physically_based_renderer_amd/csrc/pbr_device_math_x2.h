@@ -248,6 +248,15 @@ __device__ __forceinline__ v2 in_range01(v2 dist) {
     return r;
 }
 
+// The range test for spot lights: a select, not the 0/1 factor. The cone factor pow(c, SpotPower)
+// (LightingUtil.hlsl:163) can be +inf or NaN for an adversarial light (SpotPower < 0 with c = 0, a NaN
+// SpotPower, |Direction| > 1 under a huge power) that the light window does not see, and inf * 0 = NaN,
+// where the reference returns 0 before it evaluates the pow (:154). Spot lights already pay two glibc
+// powf per pair, so the select costs nothing measurable.
+__device__ __forceinline__ v2 spot_range_select(v2 att, v2 dist) {
+    return v2{dist.x > 100.0f ? 0.0f : att.x, dist.y > 100.0f ? 0.0f : att.y};
+}
+
 // ComputePointLight / ComputeSpotLight, packed fast path. The range test (exact, as in the scalar
 // version) scales the attenuation by 1 or 0 (in_range01), so an unlit lane's contribution is
 // (finite) * 0 = +-0 whenever the lane is inside the window (`ok`: every value of the fast path is then
@@ -268,8 +277,10 @@ __device__ __forceinline__ f3x2 point_or_spot_x2(const PixelInvariants2& q, cons
     if (SPOT) {
         v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
+        att = spot_range_select(att, dist);
+    } else {
+        att *= in_range01(dist);  // beyond the range: +0
     }
-    att *= in_range01(dist);  // beyond the range: +0
     return brdf_x2<LEAN>(q, f3x2{s.x * att, s.y * att, s.z * att}, l, h, ok);
 }
 
@@ -404,8 +415,10 @@ __device__ __forceinline__ void point_or_spot_faithful_x2(const PixelInvariants2
     if (SPOT) {
         const v2 c = vmax(dot3(f3x2{-l.x, -l.y, -l.z}, splat3(d.x, d.y, d.z)), splat(0.0f));
         att *= v2{powf_glibc(c.x, s.w), powf_glibc(c.y, s.w)};
+        att = spot_range_select(att, dist);
+    } else {
+        att *= in_range01(dist);  // beyond the range: +0 (see point_or_spot_x2)
     }
-    att *= in_range01(dist);  // beyond the range: +0 (see point_or_spot_x2)
     brdf_faithful_x2<LEAN, SCALED>(q, fi, s, att, l, h, ok, sum);
 }
 

@@ -52,12 +52,14 @@ def all_bands(height: int, world: int, align: int = 8) -> List[Band]:
     return [band_rows(height, world, r, align) for r in range(world)]
 
 
-def init_from_env(backend: str) -> Tuple[int, int, int]:
-    """(rank, world, local_rank) from torchrun's environment; initialises the default group once."""
+def init_from_env(backend: str, always: bool = False) -> Tuple[int, int, int]:
+    """(rank, world, local_rank) from torchrun's environment; initialises the default group once: at
+    world > 1, and at world 1 too when ``always`` (so a single-rank run exercises the same RCCL
+    communicator init / teardown and collectives as the multi-GPU one)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or always) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
         kwargs = {}
@@ -91,7 +93,7 @@ class BandGather:
         """Post the gather of ``band_out`` ((rows_max, W, 4)); returns the list of work handles."""
         b = self.band
         if b.world == 1:
-            self.frame[0].copy_(band_out)
+            self.frame[0].copy_(band_out, non_blocking=True)
             return []
         if self.host_staged:
             self._gather_host_staged(band_out)

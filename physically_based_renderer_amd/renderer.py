@@ -117,8 +117,10 @@ class GBuffer:
     def __init__(self, planes: torch.Tensor, width: Optional[int] = None):
         if planes.dim() != 3 or planes.shape[0] != N.NUM_PLANES or planes.dtype != torch.float32:
             raise ValueError("planes must be a (15, H, W) float32 tensor")
-        if planes.stride(2) != 1 or planes.stride(0) % 1 != 0:
+        if planes.stride(2) != 1:
             raise ValueError("planes rows must be contiguous")
+        if planes.stride(0) < planes.shape[1] * planes.stride(1) and planes.shape[1] > 1:
+            raise ValueError("planes must not overlap (stride(0) >= H * stride(1))")
         self.planes = planes
         self.height = planes.shape[1]
         self.width = planes.shape[2] if width is None else width
@@ -212,8 +214,17 @@ class ShadingContext:
         """Sky texture (g_SkyArray[0]) sampled for background pixels: uint16 UNORM or float32 RGBA."""
         self._set_texture("pbr_set_sky_map", texels, stream)
 
+    def _check_device(self, *tensors) -> None:
+        """Every tensor handed to the kernel must live on this context's device: a foreign pointer would be
+        dereferenced by the kernel (peer access or a fault)."""
+        want = torch.device("cuda", self.device)
+        for t in tensors:
+            if t is not None and t.device != want:
+                raise ValueError(f"tensor on {t.device}, but this ShadingContext shades on {want}")
+
     def shade(self, gb: GBuffer, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
         """Shade every pixel of ``gb`` into ``out`` ((H, >=W, 4) fp32 on the device), asynchronously."""
+        self._check_device(gb.planes, out)
         if out is None:
             out = torch.empty((gb.height, gb.width, 4), dtype=torch.float32, device=gb.planes.device)
         if out.dtype != torch.float32 or out.dim() != 3 or out.shape[2] != 4 or out.stride(2) != 1 or out.stride(1) != 4:
@@ -230,6 +241,7 @@ class ShadingContext:
                     fmt: int = N.PBR_OUTPUT_RGBA32F, stream=None) -> torch.Tensor:
         """Shade ``gb`` with the sky pass on background pixels (``coverage`` == 0; (H, >=W) uint8 on the
         device) into ``out``: (H, W, 4) float32 for RGBA32F or (H, W, 4) uint8 for RGBA8_UNORM."""
+        self._check_device(gb.planes, out, coverage)
         dev = gb.planes.device
         if fmt == N.PBR_OUTPUT_RGBA8_UNORM:
             dtype, px_bytes = torch.uint8, 4

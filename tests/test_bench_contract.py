@@ -64,8 +64,39 @@ def test_cpu_baseline_leg_checks_parity(kind):
     ops = O.OraclePass(eye=tuple(pc.eye_pos_w), ambient=tuple(pc.ambient_light), fresnel_r0=tuple(pc.fresnel_r0),
                        opacity=pc.opacity, n_point=pc.num_point_lights, ambient_mode=pc.ambient_mode)
     frame = O.shade(list(planes), ops, pc.light_array(), env, n_threads=4)  # stands in for the GPU frame
-    cpu, max_rel, exact, (step, ref) = bench.cpu_baseline(cfg, planes, pc, env, frame, 0, kind)
+    cpu, parity, (step, ref) = bench.cpu_baseline(cfg, planes, pc, env, frame, 0, kind)
     assert cpu["kind"] == ("reference" if kind == "auto" and O.ref_available() else "port")
     assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["single_thread_value"] > 0
-    assert max_rel == 0.0 and exact == 1.0 and step == 1
+    # every core of the affinity mask (capped only by a cgroup quota), with the host counts stated
+    hc = cpu["host_cpus"]
+    assert cpu["cores"] == hc["used"] and hc["affinity"] == len(os.sched_getaffinity(0))
+    assert hc["os_cpu_count"] == os.cpu_count() and hc["used"] <= hc["affinity"]
+    assert parity["parity_max_rel"] == 0.0 and parity["parity_bit_exact_frac"] == 1.0 and step == 1
     assert np.array_equal(ref.view(np.uint32), frame.view(np.uint32))
+
+
+def test_cpu_baseline_rgba8_and_gathered_parity():
+    """RGBA8 output (config 5's presented frame): the CPU leg shades in the same format and compares codes;
+    the N > 1 check refills the sampled rows of every band and compares the assembled frame."""
+    from oracle import oracle as O
+
+    cfg = S.CONFIGS[5].with_size(128, 48)
+    pc = S.scene_pass(cfg)
+    env = S.env_map()
+    planes, _ = S.fill_gbuffer_host(cfg)
+    frame8 = O.shade_frame(list(planes), bench.oracle_pass_of(pc), pc.light_array(), env, None, None,
+                           O.OUTPUT_RGBA8, n_threads=4)
+    cpu, parity, (step, ref) = bench.cpu_baseline(cfg, planes, pc, env, frame8, 0, "port", rgba8=True)
+    assert ref.dtype == np.uint8 and parity == {"parity_max_code_diff": 0, "parity_bit_exact_frac": 1.0}
+    bad = frame8.copy()
+    bad[20, 5, 1] ^= 1
+    p = bench.gathered_parity(cfg, pc, env, bad, 3, 4, rgba8=True)
+    assert p["rows_checked"] == 12 and p["parity_max_code_diff"] == 1  # band 1 = rows 16-31, sampled at 16, 20, 24, 28
+    frame32 = O.shade(list(planes), bench.oracle_pass_of(pc), pc.light_array(), env, n_threads=4)
+    p = bench.gathered_parity(cfg, pc, env, frame32, 3, 4, rgba8=False)
+    assert p["parity_max_rel"] == 0.0 and p["parity_bit_exact_frac"] == 1.0
+
+
+def test_host_cpu_budget_reads_the_quota():
+    b = bench.host_cpu_budget()
+    assert b["used"] >= 1 and b["affinity"] >= b["used"]

@@ -102,4 +102,52 @@ def test_bench_multi_rank_rehearsal(gpu):
     assert d["config"]["workload"].startswith("cfg5_8192x8192_64pt_ibl_rowbands")
     assert d["config"]["rows_per_rank"] == 64 and d["config"]["width"] == 8192
     assert d["value"] > 0 and d["cpu_baseline"] is None
-    assert d["output"] == "rgba8"  # N > 1 gathers the presented back-buffer format by default
+    assert d["output"] == "rgba8"  # config 5 gathers the presented back-buffer format by default
+    gp = d["gathered_frame_parity"]  # sampled rows of every band against the CPU oracle
+    assert gp["rows_checked"] == 4 * 8 and gp["parity_max_code_diff"] <= 1
+    assert d["shade_ms"] > 0 and d["gather_ms"] > 0
+
+
+def _bench_torchrun(nproc, extra, timeout=600):
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(nproc), "--steps", "3", "--warmup", "1", "--ramp-ms", "0"] + extra
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT,
+                       env={**os.environ, "OMP_NUM_THREADS": "2"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    return lines[0]
+
+
+def test_bench_fp32_gather_parity_multi_rank(gpu):
+    """--output rgba32f at N = 3 (gloo on the one GPU): the fp32 bands are gathered and rank 0 checks the
+    assembled frame against the CPU oracle on 8 rows of every band (faithful mode: within 1e-5)."""
+    d = _bench_torchrun(3, ["--dist-backend", "gloo", "--rows-per-rank", "64", "--output", "rgba32f"])
+    assert d["output"] == "rgba32f" and d["gather_checksums_match"] is True
+    gp = d["gathered_frame_parity"]
+    assert gp["rows_checked"] == 24 and gp["parity_max_rel"] <= 1e-5
+
+
+def test_bench_rccl_single_rank(gpu):
+    """The RCCL path that runs on a one-GPU box: torch.distributed.run with one rank creates the nccl (RCCL)
+    process group with device_id, gathers rank 0's band, runs the device-side checksum all_gather and the
+    max-over-ranks all_reduce on RCCL, and tears the communicator down -- the same calls as at N = 8."""
+    d = _bench_torchrun(1, ["--config", "5", "--rows-per-rank", "64", "--dist-backend", "nccl",
+                            "--no-cpu-baseline"])
+    assert d["process_group"] == "nccl" and d["gather_checksums_match"] is True
+    assert d["n_gpus"] == 1 and d["config"]["rows_per_rank"] == 64 and d["output"] == "rgba8"
+
+
+def test_bench_config5_one_gpu_is_the_per_rank_workload(gpu):
+    """`bench.py --gpus 1 --config 5`: the same 8192 x 1024 band and RGBA8 output each rank of the N = 8 run
+    shades (so the 1 -> 8 curve compares equal work), with the CPU leg on a row sample of that band."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", "5", "--steps",
+                        "3", "--warmup", "1", "--ramp-ms", "0", "--cpu-rows", "16", "--cpu-kind", "port"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["config"]["width"] == 8192 and d["config"]["height"] == 1024 and d["config"]["rows_per_rank"] == 1024
+    assert d["output"] == "rgba8" and d["gather_checksums_match"] is True and d["process_group"] is None
+    assert d["cpu_baseline"]["kind"] == "port" and d["parity_max_code_diff"] <= 1

@@ -390,3 +390,60 @@ def test_range_cut_at_100_on_gpu(flags, shading_ctx, gpu):
         assert O.rel_err(got, ref).max() <= REL_TOL
     assert np.array_equal(got[0, unlit].view(np.uint32), base_gpu[0, unlit].view(np.uint32))
     assert not np.any(np.all(got[0, ~unlit] == base_gpu[0, ~unlit], axis=-1))
+
+
+SPOT_ADVERSARIAL = {  # name -> (SpotPower, Direction): cone factors the light window cannot see
+    "negative_power_c0": (-2.0, (1.0, 0.0, 0.0)),      # pow(0, -2) = +inf
+    "nan_power": (float("nan"), (-0.5, 0.0, 0.0)),     # pow(0.5, NaN) = NaN
+    "non_unit_dir": (200.0, (-2.0, 0.0, 0.0)),         # pow(2, 200) = +inf in fp32
+    "unit_sharp": (64.0, (-1.0, 0.0, 0.0)),            # a well-behaved cone, for contrast
+}
+
+
+@pytest.mark.parametrize("flags", [0, N.PBR_FLAG_FAITHFUL])
+@pytest.mark.parametrize("case", sorted(SPOT_ADVERSARIAL))
+def test_spot_range_cut_with_nonfinite_cone(case, flags, shading_ctx, gpu):
+    """ComputeSpotLight returns 0 beyond d > 100 *before* its pow (LightingUtil.hlsl:154, 163), so a cone
+    factor that is inf or NaN must not leak into out-of-range pixels (inf * 0 = NaN). Pixels straddle the cut
+    at 100 + k * 2^-17; exact mode must be the oracle's bit for bit, faithful mode within 1e-5 (NaN == NaN),
+    and every pixel the oracle leaves unlit must equal the no-light frame."""
+    power, direction = SPOT_ADVERSARIAL[case]
+    w = 16
+    p = np.zeros((O.NUM_PLANES, 1, w), np.float32)
+    p[0, 0, :] = -np.arange(-8, 8, dtype=np.float32) * np.float32(2.0 ** -17)
+    p[3] = 1.0
+    p[6:9] = 0.5
+    p[10] = 0.5
+    p[11] = 1.0
+    lights = np.array([[1e3, 1e3, 1e3, power, *direction, 0, 100.0, 0, 0, 0]], np.float32)
+
+    def pass_with(n_spot):
+        return PassConstants(eye_pos_w=(50.0, 0.0, -5.0), ambient_light=(0.03, 0.03, 0.03), num_spot_lights=n_spot,
+                             flags=flags, lights_array=lights if n_spot else None)
+
+    pc = pass_with(1)
+    got = gpu_shade(shading_ctx, p, pc, None, gpu)
+    ref = O.shade(list(p), oracle_pass_from_constants(pc), pc.light_array())
+    base = gpu_shade(shading_ctx, p, pass_with(0), None, gpu)
+    base_ref = O.shade(list(p), oracle_pass_from_constants(pass_with(0)), None)
+    unlit = np.all(O.bit_equal(ref[0], base_ref[0]), axis=-1)
+    assert 0 < unlit.sum() < w
+    if flags == 0:
+        assert O.bit_equal(got, ref).all()
+    else:
+        assert O.rel_err(got, ref).max() <= REL_TOL
+    assert O.bit_equal(got[0, unlit], base[0, unlit]).all()
+
+
+def test_tensors_on_another_device_are_rejected(shading_ctx, gpu):
+    """renderer.ShadingContext hands raw pointers to the kernel: planes / out / coverage that do not live on
+    the context's device are refused before the C ABI is called."""
+    shading_ctx.set_pass(PassConstants())
+    host = GBuffer(torch.zeros((15, 8, 8)))
+    with pytest.raises(ValueError):
+        shading_ctx.shade(host)
+    dev = GBuffer(torch.zeros((15, 8, 8), device=gpu))
+    with pytest.raises(ValueError):
+        shading_ctx.shade(dev, torch.empty((8, 8, 4)))
+    with pytest.raises(ValueError):
+        shading_ctx.shade_frame(dev, coverage=torch.ones((8, 8), dtype=torch.uint8))
