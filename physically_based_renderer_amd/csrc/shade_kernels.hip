@@ -409,6 +409,16 @@ __device__ __forceinline__ bool is_geometry(const FrameArgs& fr, int x, int y) {
     return fr.coverage == nullptr || fr.coverage[(int64_t)y * fr.coverage_stride + x] != 0;
 }
 
+// The lane's index in its wave, from the hardware (v_mbcnt) in volatile asm: the compiler can neither CSE it
+// with an earlier value nor hoist it, so the pair kernel re-derives its pixel coordinates at the store
+// instead of keeping the 64-bit output offset live across the light loops (at the 128-VGPR cap of 4 waves
+// per SIMD that offset was spilled to scratch: 8 bytes written and re-read per work-item).
+__device__ __forceinline__ int lane_id_fresh() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 }  // namespace
 
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
@@ -423,6 +433,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     __syncthreads();
 
     const int tid = threadIdx.x;
+    const int wave_id = __builtin_amdgcn_readfirstlane(tid) >> 6;  // wave-uniform (SGPR)
     const int xa = blockIdx.x * kTileW + 2 * (tid & 31);
     const int y = blockIdx.y * kTileH + (tid >> 5);
     const bool va = (xa < gb.width) && (y < gb.height);
@@ -541,13 +552,16 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         tile_kept[kStatsPerBlock * t + 2] = s.exact_px;
     }
 
-    const int64_t orow = (int64_t)y * fr.out_stride;
+    // The output offset re-derived from the hardware ids (lane_id_fresh): same pixel as xa, y above.
+    const int ln = lane_id_fresh();
+    const int sx = blockIdx.x * kTileW + 2 * (ln & 31);
+    const int64_t orow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
     if (va)
-        store_pixel(fr, orow + xa, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
-                                      : sky_pixel(ua.n, ps, fr.sky, !exact_only));
+        store_pixel(fr, orow, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
+                                 : sky_pixel(ua.n, ps, fr.sky, !exact_only));
     if (vb)
-        store_pixel(fr, orow + xa + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
-                                           : sky_pixel(ub.n, ps, fr.sky, !exact_only));
+        store_pixel(fr, orow + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
+                                      : sky_pixel(ub.n, ps, fr.sky, !exact_only));
 }
 
 // ---- One pixel per work-item (32x8 tiles) ---------------------------------------------------------
