@@ -1,0 +1,394 @@
+// pbr_balanced.h -- back-face-rejected, wave-balanced point-light lists for the pair kernel.
+//
+// Why: BRDFCookTorrance returns (kD albedo / PI + spec) * radiance * max(N.L, 0) (LightingUtil.hlsl:85-104),
+// and with N.L <= 0 every factor of it is finite inside the fast-path window, so the term is +-0: adding it
+// to the running sum (which starts at +0 and is never -0) is the identity. In the BASELINE scenes about half
+// of all (pixel, light) terms are such zeros (normals uniform on the sphere), yet the uniform light loop
+// evaluates every one of them. A per-lane skip does not pay in SIMD: the number of lights that reach a pixel
+// ranges over 0..L within a wave (config 3: mean 32 of 64, max over a wave's 128 pixels ~64), so the wave
+// would still run L iterations. Instead each wave
+//   1. (pass 1) tests every (pixel, light) pair with a cheap conservative back-face test (below) and keeps a
+//      64-bit mask of the lights that may reach each of its 128 pixels;
+//   2. ranks its pixels by live-light count (LDS counting sort) and re-pairs them across lanes, the k-th
+//      smallest count with the k-th largest, moving each pixel's loop invariants through LDS;
+//   3. (pass 2) lets every lane walk its two pixels' live lights one after the other, TWO lights of the
+//      current pixel per iteration in packed fp32 (the pixel's invariants are splat operands, the two lights'
+//      records per element) -- the cycles of one packed pair-loop iteration for two items, ~L/4 iterations
+//      per pixel instead of L/2 pair iterations, and all lanes finish together (a scalar one-item loop costs
+//      the same VALU cycles per item as a packed two-item one on gfx950, measured: 1.32 vs 1.14 ms);
+//   4. hands each pixel's sum back to the lane that owns it (LDS), which finishes the pixel as before.
+// Every pixel's live lights are summed by one lane, in two interleaved partial sums (even and odd live
+// lights) added at the end: a different association than the reference's, inside the faithful bound
+// (non-negative terms).
+//
+// The back-face test (pass 1) for light j and pixel P, with l = Light.Position - P as the reference forms it:
+//   skip  <=>  t1 = N.l + c |N|_1 B_j < 0     (c = 2^-18, N.l by FMAs)
+// where B_j >= |l| for every pixel of the wave: the L1 distance from the light to the centre of the wave's
+// position box plus the box's L1 half-extent, with margins for their roundings (computed once per wave, one
+// lane per light). t1 < 0 bounds the reference's max(dot(N, L), 0) (L = l / length(l), HLSL dot) to 0: the
+// rounding error of N.l here is <= 3u sum|N_i l_i| and that of the reference's dot(N, L) <= ~9u |N|_1
+// (u = 2^-24), both far below c |N|_1 = 64u |N|_1 (N.l < -c |N|_1 B_j <= -c |N|_1 |l|). With N.L = 0 the reference's term is +-0 whatever H is: where
+// V + L = 0 its H = normalize(V + L) is NaN, but max(dot(N, H), 0) and saturate(dot(H, V)) map NaN to 0 (IEEE
+// maxNum, LightingUtil.hlsl:55, 45), so NDF and F stay finite and G = 0. Every other factor is finite for a
+// pixel and light inside the fast-path window (the lean-wave bounds of brdf_x2: den in [2^-37, PI], F0 window;
+// attenuation <= 1e4). l == 0 (pixel on the light: 0 / 0 in the reference) keeps the item live through the
+// 2^-120 seed of the N.l chain. So every skipped term is +-0 in the reference and needs no window test; live
+// items run the usual window tests (the plain loop also sends pixels with |V + L| < 2^-30 to the exact
+// re-pass; here that happens only when such an item is live). Lights whose fast-path flag is off
+// (pbr_set_pass) make the host choose the uniform loop (PassArgs::balanced), which sends every pixel to the
+// exact re-pass.
+#pragma once
+#include <cstdint>
+
+#include "pbr_device_math.h"
+#include "pbr_device_math_x2.h"
+#include "shade_kernels.h"
+
+namespace pbr {
+
+constexpr int kBalRec = 7;         // float4 per exchanged pixel record
+
+// Per-wave LDS: the exchange region (one record per lane, then the 128 results) and the count histogram.
+#ifndef PBR_BAL_EXPERIMENT
+#define PBR_BAL_EXPERIMENT 0  // development timing switches (0 = product)
+#endif
+#ifndef PBR_BAL_PROFILE
+#define PBR_BAL_PROFILE 0  // development build: per-phase shader-clock sums (pbr_debug_bal_profile)
+#endif
+#if PBR_BAL_PROFILE
+// [0] pass 1, [1] rank + exchange, [2] pass 2, [3] hand-back, [4] waves, [5] pass-2 iterations,
+// [6] whole kernel (entry to the stores), [7] entry to the light loop, [8] light loop end to the reloaded
+// invariants, [9] to after the exact re-pass barrier, [10] to the stores
+__device__ unsigned long long g_bal_prof[16];
+#define BAL_PROF_T(v) const long long v = (long long)__builtin_amdgcn_s_memtime()
+#define BAL_PROF_ADD(slot_, val_) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_bal_prof[slot_], (unsigned long long)(val_)); } while (0)
+#else
+#define BAL_PROF_T(v)
+#define BAL_PROF_ADD(i, x)
+#endif
+
+// The pass's point lights in LDS, structure of arrays (px, py, pz, sx, sy, sz): pass 1 reads four lights'
+// coordinates with one broadcast ds_read_b128 per array, pass 2's two elements read straight into a register
+// pair. Entries [n, kBalLdsStride) are zero: pass 1 may test a padded light (its bit is masked off) and entry
+// kBalMaxLights is the zero strength of an iteration's second element when one light is left.
+constexpr int kBalLdsStride = kBalMaxLights + 4;  // 68 floats: every array 16-byte aligned
+__device__ __forceinline__ void stage_balanced_lights(const float4* __restrict__ lights, int b0, int b1,
+                                                      float* lds_lights) {
+    const int t = (int)threadIdx.x;
+    if (t < kBalLdsStride) {
+        float4 p = make_float4(0.0f, 0.0f, 0.0f, 0.0f), st = p;
+        if (t < b1 - b0) {
+            p = lights[3 * (b0 + t) + 2];
+            st = lights[3 * (b0 + t)];
+        }
+        lds_lights[0 * kBalLdsStride + t] = p.x;
+        lds_lights[1 * kBalLdsStride + t] = p.y;
+        lds_lights[2 * kBalLdsStride + t] = p.z;
+        lds_lights[3 * kBalLdsStride + t] = st.x;
+        lds_lights[4 * kBalLdsStride + t] = st.y;
+        lds_lights[5 * kBalLdsStride + t] = st.z;
+    }
+}
+
+struct BalancedWaveLds {
+    float4 rec[64 * kBalRec];  // 7 KiB
+    float4 bound[16];          // pass 1: the lights' distance bounds B_j (64 floats)
+    int hist[64];
+};
+
+// The per-pixel loop invariants of the faithful scaled lean loop (the scalar view of PixelInvariants2 after
+// faithful_scale plus Faithful2), the pixel's live-light mask and where it came from.
+struct ItemPixel {
+    f3 pos, n, v, f0, omf0, mab;
+    float a2m1, k, omk, nv, a2gv;
+    uint32_t live0, live1;  // lights [0, 32) and [32, 64) of the pass: bit j % 32
+    int origin;             // owner lane * 2 + element
+};
+
+__device__ __forceinline__ ItemPixel item_pixel(const PixelInvariants2& q, const Faithful2& fi, const f3x2& pos, int e,
+                                                uint32_t live0, uint32_t live1, int origin) {
+    ItemPixel r;
+    r.pos = lane(pos, e);
+    r.n = lane(q.n, e);
+    r.v = lane(q.v, e);
+    r.f0 = lane(q.f0, e);
+    r.omf0 = lane(q.one_minus_f0, e);
+    r.mab = lane(fi.mabpi, e);
+    r.a2m1 = e ? q.a_sqr_minus_1.y : q.a_sqr_minus_1.x;
+    r.k = e ? q.k.y : q.k.x;
+    r.omk = e ? q.one_minus_k.y : q.one_minus_k.x;
+    r.nv = e ? q.four_n_dot_v.y : q.four_n_dot_v.x;
+    r.a2gv = e ? fi.a2gv.y : fi.a2gv.x;
+    r.live0 = live0;
+    r.live1 = live1;
+    r.origin = origin;
+    return r;
+}
+
+__device__ __forceinline__ void store_item(float4* dst, const ItemPixel& p) {
+    dst[0] = make_float4(p.pos.x, p.pos.y, p.pos.z, p.n.x);
+    dst[1] = make_float4(p.n.y, p.n.z, p.v.x, p.v.y);
+    dst[2] = make_float4(p.v.z, p.f0.x, p.f0.y, p.f0.z);
+    dst[3] = make_float4(p.omf0.x, p.omf0.y, p.omf0.z, p.mab.x);
+    dst[4] = make_float4(p.mab.y, p.mab.z, p.a2m1, p.k);
+    dst[5] = make_float4(p.omk, p.nv, p.a2gv, __uint_as_float(p.live0));
+    dst[6] = make_float4(__uint_as_float(p.live1), __int_as_float(p.origin), 0.0f, 0.0f);
+}
+__device__ __forceinline__ ItemPixel load_item(const float4* src) {
+    const float4 a = src[0], b = src[1], c = src[2], d = src[3], e = src[4], f = src[5], g = src[6];
+    ItemPixel p;
+    p.pos = mk3(a.x, a.y, a.z);
+    p.n = mk3(a.w, b.x, b.y);
+    p.v = mk3(b.z, b.w, c.x);
+    p.f0 = mk3(c.y, c.z, c.w);
+    p.omf0 = mk3(d.x, d.y, d.z);
+    p.mab = mk3(d.w, e.x, e.y);
+    p.a2m1 = e.z;
+    p.k = e.w;
+    p.omk = f.x;
+    p.nv = f.y;
+    p.a2gv = f.z;
+    p.live0 = __float_as_uint(f.w);
+    p.live1 = __float_as_uint(g.x);
+    p.origin = __float_as_int(g.y);
+    return p;
+}
+
+// LDS traffic of one wave between its own lanes: the hardware executes a wave's LDS instructions in order;
+// the fences keep the compiler from moving them across this point.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float bal_wave_min(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ float bal_wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// Pass 1 for the pair and one light (position lx, ly, lz, distance bound bj): shift the light's SKIP bit for
+// each pixel (the sign of t1, see the header comment) into `ma` / `mb` (bit 31 after this call).
+__device__ __forceinline__ void push_skip_bits(uint32_t& ma, uint32_t& mb, float lx, float ly, float lz, float bj,
+                                               const f3x2& pos, const f3x2& n, v2 cn) {
+    const f3x2 l = f3x2{lx - pos.x, ly - pos.y, lz - pos.z};  // LightingUtil.hlsl:127
+    const v2 nl = vfma(n.z, l.z, vfma(n.y, l.y, vfma(n.x, l.x, splat(0x1p-120f))));
+    const v2 t1 = vfma(cn, splat(bj), nl);
+    ma = __builtin_amdgcn_alignbit(ma, __float_as_uint(t1.x), 31);  // (m << 1) | sign(t1)
+    mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(t1.y), 31);
+}
+
+// ---- pass 2: two (pixel, light) items of the faithful scaled lean loop, packed ---------------------------
+// ComputePointLight (LightingUtil.hlsl:124-142) + BRDFCookTorrance for ONE pixel (q, splat into both elements)
+// and TWO lights (element e: position lp.*[e], strength ls.*[e]), added into `sum`: the operations of
+// point_or_spot_faithful_x2<false, true, true> / brdf_faithful_x2<true, true> element for element (same
+// roundings, same window tests into `ok`).
+__device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const f3x2& lp, const f3x2& ls, m2& ok,
+                                                      f3x2& sum) {
+    f3x2 l = f3x2{lp.x - q.pos.x, lp.y - q.pos.y, lp.z - q.pos.z};
+    const v2 dist = sqrt_nr(dot3(l, l));
+    ok &= ge(dist, 0.01f);
+    const Recip2 rdist = recip_nr(dist);
+    l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
+    const f3x2 h = normalize_x2(f3x2{q.v.x + l.x, q.v.y + l.y, q.v.z + l.z}, ok);
+    const v2 att = (rdist.r * rdist.r) * in_range01(dist);
+    const f3x2 n = splat3(q.n.x, q.n.y, q.n.z);
+    const v2 n_dot_h = dot3_sat(n, h);
+    const v2 inner = ((n_dot_h * n_dot_h) * q.a2m1 + 1.0f);
+    const v2 den = inner * inner;
+    const v2 n_dot_l = dot3_sat(n, l);
+    const v2 r = rcp_hw((den * vfma(n_dot_l, splat(q.omk), splat(q.k))) * vfma(splat(q.nv), n_dot_l, splat(0.001f)));
+    const v2 p = pow5_faithful(1.0f - dot3_sat(h, splat3(q.v.x, q.v.y, q.v.z)));
+    const f3x2 f = f3x2{q.f0.x + q.omf0.x * p, q.f0.y + q.omf0.y * p, q.f0.z + q.omf0.z * p};
+    const v2 kr = (q.a2gv * n_dot_l) * r;
+    const v2 w = att * n_dot_l;
+    sum.x = vfma(vfma(kr, f.x, vfma(-f.x, splat(q.mab.x), splat(q.mab.x))), ls.x * w, sum.x);
+    sum.y = vfma(vfma(kr, f.y, vfma(-f.y, splat(q.mab.y), splat(q.mab.y))), ls.y * w, sum.y);
+    sum.z = vfma(vfma(kr, f.z, vfma(-f.z, splat(q.mab.z), splat(q.mab.z))), ls.z * w, sum.z);
+}
+
+// The whole balanced pass over point lights [b0, b1) (b1 - b0 <= kBalMaxLights) of an untiled faithful lean
+// wave. q / fi are the pair's scaled invariants (faithful_scale), `live_a` / `live_b` say which of the pair's
+// pixels take part (geometry). Adds each pixel's point-light sum into `sum` (any order is within the faithful
+// bound) and ORs the pixels that left the fast-path window into `redo`. Wave-uniform control
+// flow; no block barrier.
+// `lds_lights`: the pass's point lights [b0, b1) staged by the block (stage_balanced_lights).
+__device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2& q, const Faithful2& fi,
+                                                         const f3x2& pos, bool live_a, bool live_b,
+                                                         const float4* __restrict__ lights, int b0, int b1,
+                                                         BalancedWaveLds& w, const float* lds_lights, f3x2& sum,
+                                                         m2& redo) {
+    const int lane_id = (int)(threadIdx.x & 63);
+    const int n = b1 - b0;
+    BAL_PROF_T(t0);
+    // ---- pass 1: live masks of both pixels
+    // The wave's position box (geometry pixels) -> centre c and L1 half-extent r; lane k computes light k's
+    // bound B_k = (|p_k - c|_1 + r + |c|_1 2^-22) (1 + 2^-20) >= |p_k - P|_1 >= |p_k - P| for every pixel P of
+    // the wave (the extra terms cover the roundings of c, r and B_k) into the wave's LDS region.
+    const float big = 3.0e38f;
+    const f3 pa = lane(pos, 0), pb = lane(pos, 1);
+    const float mnx = bal_wave_min(fminf(live_a ? pa.x : big, live_b ? pb.x : big));
+    const float mny = bal_wave_min(fminf(live_a ? pa.y : big, live_b ? pb.y : big));
+    const float mnz = bal_wave_min(fminf(live_a ? pa.z : big, live_b ? pb.z : big));
+    const float mxx = bal_wave_max(fmaxf(live_a ? pa.x : -big, live_b ? pb.x : -big));
+    const float mxy = bal_wave_max(fmaxf(live_a ? pa.y : -big, live_b ? pb.y : -big));
+    const float mxz = bal_wave_max(fmaxf(live_a ? pa.z : -big, live_b ? pb.z : -big));
+    const float cx = 0.5f * mnx + 0.5f * mxx, cy = 0.5f * mny + 0.5f * mxy, cz = 0.5f * mnz + 0.5f * mxz;
+    const float r = (0.5f * (mxx - mnx) + 0.5f * (mxy - mny)) + 0.5f * (mxz - mnz);
+    const float slack = r + (fabsf(cx) + fabsf(cy) + fabsf(cz)) * 0x1p-22f;
+    if (lane_id < kBalLdsStride - 4) {  // B_j for j < n; padded lights (zero position) get a bound too
+        const float lx = lds_lights[lane_id], ly = lds_lights[kBalLdsStride + lane_id],
+                    lz = lds_lights[2 * kBalLdsStride + lane_id];
+        reinterpret_cast<float*>(w.bound)[lane_id] =
+            (((fabsf(lx - cx) + fabsf(ly - cy)) + fabsf(lz - cz)) + slack) * (1.0f + 0x1p-20f);
+    }
+    wave_lds_sync();
+    const v2 cn = v2{0x1p-18f * ((fabsf(q.n.x.x) + fabsf(q.n.y.x)) + fabsf(q.n.z.x)),
+                     0x1p-18f * ((fabsf(q.n.x.y) + fabsf(q.n.y.y)) + fabsf(q.n.z.y))};
+    uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // skip bits; pixel a: a0 (lights 0..31), a1; pixel b: c0, c1
+    // Four lights per step from uniform (broadcast) LDS reads, pushed from the highest light down so that
+    // light j ends at bit j % 32 of its word; the top step of a word may test padded lights (masked below).
+    const float4* px4 = reinterpret_cast<const float4*>(lds_lights);
+    const float4* py4 = reinterpret_cast<const float4*>(lds_lights + kBalLdsStride);
+    const float4* pz4 = reinterpret_cast<const float4*>(lds_lights + 2 * kBalLdsStride);
+    auto word = [&](int lo, int hi, uint32_t& ma, uint32_t& mb) {  // lights [lo, hi), hi - lo <= 32
+        for (int q4 = (hi - 1) >> 2; q4 >= (lo >> 2); --q4) {
+            const float4 x = px4[q4], y = py4[q4], z = pz4[q4], b = w.bound[q4];
+            push_skip_bits(ma, mb, x.w, y.w, z.w, b.w, pos, q.n, cn);
+            push_skip_bits(ma, mb, x.z, y.z, z.z, b.z, pos, q.n, cn);
+            push_skip_bits(ma, mb, x.y, y.y, z.y, b.y, pos, q.n, cn);
+            push_skip_bits(ma, mb, x.x, y.x, z.x, b.x, pos, q.n, cn);
+        }
+    };
+    const int n0 = n < 32 ? n : 32;
+    if (n > 32) word(32, n, a1, c1);
+    word(0, n0, a0, c0);
+    // Live masks (light j at bit j % 32 of its word); bits above a word's light count are not lights.
+    const int n1 = n - n0;
+    const uint32_t k0 = n0 == 32 ? ~0u : (1u << n0) - 1u, k1 = n1 == 32 ? ~0u : (1u << n1) - 1u;
+    a0 = live_a ? ~a0 & k0 : 0u;
+    c0 = live_b ? ~c0 & k0 : 0u;
+    a1 = live_a ? ~a1 & k1 : 0u;
+    c1 = live_b ? ~c1 & k1 : 0u;
+
+    BAL_PROF_T(t1);
+    // ---- rank the wave's 128 pixels by live count (counting sort; ties in LDS-atomic order, which only
+    // decides which lane evaluates a pixel, never how)
+    const int cnt_a = __popc(a0) + __popc(a1), cnt_b = __popc(c0) + __popc(c1);
+    w.hist[lane_id] = 0;
+    wave_lds_sync();
+    const int bin_a = cnt_a < 63 ? cnt_a : 63, bin_b = cnt_b < 63 ? cnt_b : 63;
+    const int pos_a = atomicAdd(&w.hist[bin_a], 1);
+    const int pos_b = atomicAdd(&w.hist[bin_b], 1);
+    wave_lds_sync();
+    const int h = w.hist[lane_id];
+    int incl = h;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off, 64);
+        if (lane_id >= off) incl += t;
+    }
+    wave_lds_sync();
+    w.hist[lane_id] = incl - h;  // exclusive prefix: first rank of each bin
+    wave_lds_sync();
+    const int rank_a = w.hist[bin_a] + pos_a, rank_b = w.hist[bin_b] + pos_b;
+    // rank r < 64 -> lane r, first pixel; r >= 64 -> lane 127 - r, second pixel.
+    const ItemPixel ia = item_pixel(q, fi, pos, 0, a0, a1, 2 * lane_id);
+    const ItemPixel ib = item_pixel(q, fi, pos, 1, c0, c1, 2 * lane_id + 1);
+    // Phase 0: the small-count pixels.
+    if (rank_a < 64) store_item(&w.rec[kBalRec * rank_a], ia);
+    if (rank_b < 64) store_item(&w.rec[kBalRec * rank_b], ib);
+    wave_lds_sync();
+    ItemPixel cur = load_item(&w.rec[kBalRec * lane_id]);
+    wave_lds_sync();
+    // Phase 1: the large-count pixels stay in LDS; a lane reads its second pixel when it switches.
+    if (rank_a >= 64) store_item(&w.rec[kBalRec * (127 - rank_a)], ia);
+    if (rank_b >= 64) store_item(&w.rec[kBalRec * (127 - rank_b)], ib);
+    wave_lds_sync();
+
+    BAL_PROF_T(t2);
+    // ---- pass 2
+    // Window results are per-lane bools here: the loop body runs under a partial exec mask, where a lane
+    // mask (m2, a ballot) has no bits for the inactive lanes -- ANDing it into a running mask would clear them.
+    f3x2 acc = splat3(0.0f, 0.0f, 0.0f);
+    f3 acc_first = mk3(0.0f, 0.0f, 0.0f);
+    bool ok = true, ok_first = true;
+    int origin_first = cur.origin;
+    bool second = false;
+    uint64_t m = ((uint64_t)cur.live1 << 32) | cur.live0;
+    auto next_pixel = [&]() {  // divergent: the lanes whose first pixel is done
+        acc_first = mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
+        ok_first = ok;
+        origin_first = cur.origin;
+        cur = load_item(&w.rec[kBalRec * lane_id]);
+        m = ((uint64_t)cur.live1 << 32) | cur.live0;
+        acc = splat3(0.0f, 0.0f, 0.0f);
+        ok = true;
+        second = true;
+    };
+    if (m == 0) next_pixel();
+#if PBR_BAL_EXPERIMENT == 1  // timing experiment: no pass 2
+    m = 0;
+    if (!second) next_pixel();
+    m = 0;
+#endif
+#if PBR_BAL_PROFILE
+    int iters = 0;
+#endif
+    while (true) {
+        const bool active = m != 0;
+        if (__builtin_amdgcn_ballot_w64(active) == 0) break;
+#if PBR_BAL_PROFILE
+        ++iters;
+#endif
+        if (active) {
+            const int j0 = __builtin_ctzll(m);
+            m &= m - 1;
+            const bool two = m != 0;
+            const int j1 = two ? __builtin_ctzll(m) : j0;  // one light left: the second element repeats it ...
+            m &= two ? m - 1 : m;
+            const int s1 = two ? j1 : kBalMaxLights;         // ... with the zero strength: it adds +0
+            m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests; only this lane's bits are read
+            const float* L = lds_lights;
+            constexpr int S = kBalLdsStride;
+            faithful_point_items2(cur, f3x2{v2{L[j0], L[j1]}, v2{L[S + j0], L[S + j1]}, v2{L[2 * S + j0], L[2 * S + j1]}},
+                                  f3x2{v2{L[3 * S + j0], L[3 * S + s1]}, v2{L[4 * S + j0], L[4 * S + s1]},
+                                       v2{L[5 * S + j0], L[5 * S + s1]}},
+                                  oki, acc);
+            ok = ok && on(oki.x) && on(oki.y);
+            if (m == 0 && !second) next_pixel();
+        }
+    }
+    BAL_PROF_T(t3);
+    const f3 acc_second = mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
+    const bool ok_second = ok;
+    // Every lane is on its second pixel now: a lane switches when its first pixel has no live light left,
+    // and the loop runs until no lane has one.
+    const int origin_second = cur.origin;
+    wave_lds_sync();
+    // ---- hand the sums back: results at rec[origin] (128 float4), owner reads its two
+    w.rec[origin_first] = make_float4(acc_first.x, acc_first.y, acc_first.z, ok_first ? 1.0f : 0.0f);
+    w.rec[origin_second] = make_float4(acc_second.x, acc_second.y, acc_second.z, ok_second ? 1.0f : 0.0f);
+    wave_lds_sync();
+    const float4 ra = w.rec[2 * lane_id], rb = w.rec[2 * lane_id + 1];
+    wave_lds_sync();
+    sum = f3x2{sum.x + v2{ra.x, rb.x}, sum.y + v2{ra.y, rb.y}, sum.z + v2{ra.z, rb.z}};
+    redo |= mask2(live_a && ra.w == 0.0f, live_b && rb.w == 0.0f);
+#if PBR_BAL_PROFILE
+    BAL_PROF_T(t4);
+    BAL_PROF_ADD(0, t1 - t0);
+    BAL_PROF_ADD(1, t2 - t1);
+    BAL_PROF_ADD(2, t3 - t2);
+    BAL_PROF_ADD(3, t4 - t3);
+    BAL_PROF_ADD(4, 1);
+    BAL_PROF_ADD(5, iters);
+#endif
+}
+
+}  // namespace pbr

@@ -48,6 +48,10 @@ struct pbr_context {
     int64_t tile_kept_capacity = 0;
     int64_t last_tiles = 0;
     bool last_culled = false;
+    // Wave-balanced point-light lists (pbr_balanced.h) for untiled faithful passes with at least this many
+    // point lights and no spot lights; PBR_BALANCED_MIN overrides (0 disables).
+    int balanced_min = 16;
+    bool points_flag_ok = false;  // pbr_set_pass: every point light inside the fast-path window
     int pixels_per_thread = 2;  // kernel layout: packed pixel pairs (measured faster); PBR_PIXELS_PER_THREAD=1 overrides
     std::string last_error;
     std::mutex mu;
@@ -108,6 +112,7 @@ int pbr_context_create(int device, pbr_context** out_ctx) {
     if (!ctx) return PBR_ERR_OUT_OF_MEMORY;
     ctx->device = device;
     if (const char* e = std::getenv("PBR_PIXELS_PER_THREAD")) ctx->pixels_per_thread = std::atoi(e) == 1 ? 1 : 2;
+    if (const char* e = std::getenv("PBR_BALANCED_MIN")) ctx->balanced_min = std::atoi(e);
     DeviceGuard g(device);
     if (!g.ok) {
         delete ctx;
@@ -179,6 +184,7 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
         if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass hipMalloc");
         ctx->lights_capacity = cap;
     }
+    bool points_ok = true;  // every point light's fast-path flag is set (the balanced pass needs it)
     if (n > 0) {
         const int slot = ctx->ring_next;
         ctx->ring_next = (slot + 1) % pbr_context::kRing;
@@ -205,6 +211,7 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
                 if (!directional) ok = ok && std::isfinite(L.strength[k]);
             }
             L.pad1 = ok ? 1.0f : 0.0f;
+            if (i >= nd && i < nd + np) points_ok = points_ok && ok;
         }
         e = hipMemcpyAsync(ctx->d_lights, ctx->h_ring[slot], sizeof(pbr_light) * (size_t)n, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass copy");
@@ -238,6 +245,7 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
     if (pass->ambient_mode == PBR_AMBIENT_CONSTANT)
         for (int k = 0; k < 3; ++k) nonneg = nonneg && pass->ambient_light[k] >= 0.0f;
     ctx->faithful_pass_ok = nonneg;
+    ctx->points_flag_ok = points_ok;
     ctx->ambient_mode = pass->ambient_mode;
     ctx->flags = pass->flags;
     ctx->pass_set = true;
@@ -355,6 +363,9 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
                     (ctx->ambient_mode != PBR_AMBIENT_IBL_DIFFUSE || ctx->env.nonneg);
     if (a.ps.faithful && ctx->faithful_count_terms) a.ps.faithful = 2;
     a.pixels_per_thread = ctx->pixels_per_thread;
+    a.ps.balanced = a.ps.faithful == 1 && !cull && a.pixels_per_thread == 2 && ctx->balanced_min > 0 &&
+                    ctx->points_flag_ok &&
+                    a.ps.n_spot == 0 && a.ps.n_point >= ctx->balanced_min && a.ps.n_point <= pbr::kBalMaxLights;
 
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;
@@ -469,3 +480,8 @@ int pbr_last_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream) {
 }
 
 }  // extern "C"
+
+// Development: the balanced pass's per-phase clock sums of a PBR_BAL_PROFILE build (not in the public header).
+extern "C" int pbr_debug_bal_profile(unsigned long long* out8, int reset) {
+    return pbr::debug_bal_profile(out8, reset != 0) == hipSuccess ? 0 : -1;
+}

@@ -28,6 +28,7 @@ struct PassArgs {
     int env_w, env_h;
     int sky_w, sky_h;
     int eye_ok;  // the eye position is inside the fast-path window (0 or |x| in [2^-20, 2^20]), host-checked
+    int balanced;  // untiled faithful pass whose point lights take the wave-balanced lists (pbr_balanced.h)
     int faithful;  // PBR_FLAG_FAITHFUL: 0 off; 1 on (host preconditions hold); 2 on, culled pass with > 64
                    // lights: the kernel counts each wave's summed terms against the bound's 64
 };
@@ -46,6 +47,7 @@ struct FrameArgs {
 };
 
 constexpr int kStatsPerBlock = 3;
+constexpr int kBalMaxLights = 64;  // point lights per wave-balanced pass (one 64-bit live mask per pixel)
 
 struct LaunchArgs {
     GBufferArgs gb;
@@ -68,6 +70,7 @@ struct LaunchArgs {
 hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);
 // Number of tiles (workgroups) launch_shade uses for a width x height G-buffer.
 int64_t shade_tile_count(int width, int height, int pixels_per_thread);
+hipError_t debug_bal_profile(unsigned long long* out8, bool reset);  // PBR_BAL_PROFILE builds only
 hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream);
 
 }  // namespace pbr

@@ -26,6 +26,7 @@
 
 #include "pbr_device_math.h"
 #include "pbr_device_math_x2.h"
+#include "pbr_balanced.h"
 #include "shade_kernels.h"
 
 namespace pbr {
@@ -61,7 +62,13 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 struct Lds {
-    float4 light[3 * kChunk];
+    union {
+        float4 light[3 * kChunk];  // the exact re-pass's staged lights
+        struct {                   // the balanced point-light pass (pbr_balanced.h)
+            BalancedWaveLds bal[kBlock / 64];        // one exchange region per wave
+            float bal_light[6 * kBalLdsStride];      // the pass's point lights (stage_balanced_lights)
+        };
+    };
     int wave_cnt[kBlock / 64];
     float bounds[kBlock / 64][6];
     int kept_sum, geo_waves;  // tiled-culling statistics of the block
@@ -172,10 +179,14 @@ __device__ __forceinline__ int wave_light_terms(const float4* __restrict__ light
 // increasing bit order, so the kept lights are summed in the reference's order. A dropped light is
 // one the reference's `d > 100` test (LightingUtil.hlsl:131) rejects for every pixel of the wave, i.e.
 // a +0 term: the result is bit-identical to the unculled pass.
-template <bool CULL, bool LEAN, bool FAITHFUL = false>
+// BALANCED (untiled faithful lean waves, ps.balanced): the point lights run through the back-face-rejected,
+// wave-balanced lists of pbr_balanced.h (region `bal`; `geo_a` / `geo_b`: the pair's geometry pixels).
+template <bool CULL, bool LEAN, bool FAITHFUL = false, bool BALANCED = false>
 __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f3x2& pos, m2 fast_ok,
                                               const float4* __restrict__ lights, const PassArgs& ps,
-                                              const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total) {
+                                              const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total,
+                                              BalancedWaveLds* bal = nullptr, const float* bal_lights = nullptr,
+                                              bool geo_a = false, bool geo_b = false) {
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     Faithful2 fi{};
     if (FAITHFUL) fi = make_faithful<!CULL>(q);
@@ -225,8 +236,13 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
             }
         }
     };
-    run_kind(std::false_type{}, pt_begin, sp_begin);
-    if (end > sp_begin) run_kind(std::true_type{}, sp_begin, end);
+    // BALANCED passes have no spot lights (host: PassArgs::balanced): nothing reads q or pos after the
+    // balanced loop, so the caller can drop them across it.
+    if (BALANCED)
+        lighting_balanced_points(q, fi, pos, geo_a, geo_b, lights, pt_begin, sp_begin, *bal, bal_lights, direct, redo);
+    else
+        run_kind(std::false_type{}, pt_begin, sp_begin);
+    if (!BALANCED && end > sp_begin) run_kind(std::true_type{}, sp_begin, end);
     if (FAITHFUL) {
         // The faithful loop's relative bound holds for sums of normal-range values: a nonzero sum
         // outside [2^-100, 2^100] (tiny sums, where underflowed terms -- a spot cone's pow, say -- carry
@@ -330,6 +346,21 @@ __device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArg
     return p;
 }
 
+// V = normalize(g_CameraPosW - pin.PosW) (Default.hlsl:53) and the BRDF invariants of the pair. In the window
+// every component of eye - pos is 0 or >= 2^-44 and |eye - pos| < 2^22, so the exact fast normalize applies
+// once |V| >= 2^-30; other pixels take the IEEE sequences.
+__device__ __forceinline__ PixelInvariants2 pair_invariants(const PairIn& p, const PassArgs& ps, m2 fast2) {
+    const f3x2 ve = f3x2{ps.eye[0] - p.pos.x, ps.eye[1] - p.pos.y, ps.eye[2] - p.pos.z};
+    m2 okv = fast2;
+    f3x2 v = normalize_x2(ve, okv);
+    const bool va_ok = on(okv.x), vb_ok = on(okv.y);
+    if (__builtin_expect(!(va_ok && vb_ok), 0)) {
+        const f3 v0 = va_ok ? lane(v, 0) : normalize3(lane(ve, 0)), v1 = vb_ok ? lane(v, 1) : normalize3(lane(ve, 1));
+        v = f3x2{v2{v0.x, v1.x}, v2{v0.y, v1.y}, v2{v0.z, v1.z}};
+    }
+    return make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness, fast2);
+}
+
 // Ambient + tonemap + gamma for one pixel (Default.hlsl:139-160), returns the output RGBA.
 // Reinhard c / (c + 1) (Default.hlsl:153, Skybox.hlsl:47): the Markstein step when `fast` and c is 0 or
 // in [2^-100, 2^60] (then c + 1 is in [1, 2^60]); the IEEE division otherwise.
@@ -421,15 +452,21 @@ __device__ __forceinline__ int lane_id_fresh() {
 
 }  // namespace
 
-template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
+// BAL (untiled only): the variant whose faithful lean waves take the wave-balanced point-light lists
+// (pbr_balanced.h); a separate instantiation so that the other variants' register allocation is untouched.
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, bool BAL = false>
 __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GBufferArgs gb, PassArgs ps,
                                                             const float4* __restrict__ lights,
                                                             const float4* __restrict__ env, FrameArgs fr,
                                                             int32_t* __restrict__ tile_kept,
                                                             bool exact_only) {
     __shared__ Lds s;
+#if PBR_BAL_PROFILE
+    const long long t_entry = (long long)__builtin_amdgcn_s_memtime();
+#endif
     load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
     if (threadIdx.x == 0) s.kept_sum = s.geo_waves = s.exact_px = 0;
+    if constexpr (BAL) stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light);
     __syncthreads();
 
     const int tid = threadIdx.x;
@@ -444,8 +481,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const bool ga = va && is_geometry(fr, xa, y), gb_ = vb && is_geometry(fr, xa + 1, y);
     const bool wave_geometry = lanes(ga || gb_) != 0;  // waves wholly outside the frame skip lighting
 
-    const PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
-                                                   vb && gb.pairs_aligned);
+    PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
+                                             vb && gb.pairs_aligned);
     const f3 pa = lane(p.pos, 0), pb = lane(p.pos, 1);
 
     const bool ok_a = !exact_only && ps.eye_ok && fast_window_ok(pa, lane(p.n, 0), lane(p.albedo, 0), lane(p.f0, 0),
@@ -454,18 +491,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                     p.metallic.y, p.roughness.y);
     const m2 fast2 = mask2(ok_a, ok_b);
 
-    // V = normalize(g_CameraPosW - pin.PosW)  (Default.hlsl:53). In the window every component of
-    // eye - pos is 0 or >= 2^-44 and |eye - pos| < 2^22, so the exact fast normalize applies once
-    // |V| >= 2^-30; other pixels take the IEEE sequences.
-    const f3x2 ve = f3x2{ps.eye[0] - p.pos.x, ps.eye[1] - p.pos.y, ps.eye[2] - p.pos.z};
-    m2 okv = fast2;
-    f3x2 v = normalize_x2(ve, okv);
-    const bool va_ok = on(okv.x), vb_ok = on(okv.y);
-    if (__builtin_expect(!(va_ok && vb_ok), 0)) {
-        const f3 v0 = va_ok ? lane(v, 0) : normalize3(lane(ve, 0)), v1 = vb_ok ? lane(v, 1) : normalize3(lane(ve, 1));
-        v = f3x2{v2{v0.x, v1.x}, v2{v0.y, v1.y}, v2{v0.z, v1.z}};
-    }
-    PixelInvariants2 q2 = make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness, fast2);
+    PixelInvariants2 q2 = pair_invariants(p, ps, fast2);
 
     // The wave's world-space box (its 64x2 pixels; background pixels excluded): wave64 butterflies,
     // then scalar registers. Non-finite positions disable culling for the wave (the reference's
@@ -490,8 +516,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     // loop does not carry two copies of the invariants.
     int kept_total = 0;
     m2 redo = m2{0, 0};
-    const f3x2 pos2 = p.pos;
-    const float ao_a = p.ao.x, ao_b = p.ao.y;
+    f3x2 pos2 = p.pos;
+    float ao_a = p.ao.x, ao_b = p.ao.y;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
     bool faithful_wave = false;  // wave-uniform: the faithful loop ran, so the finish may be faithful too
     if (wave_geometry) {  // wave-uniform
@@ -516,8 +542,41 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         // Untiled faithful waves read rescaled invariants (exact both ways, faithful_scale).
         if (faithful_wave && lean_wave) {
             if (!CULL) faithful_scale(q2);
-            d2 = lighting_fast<CULL, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
-            if (!CULL) faithful_unscale(q2);
+            if constexpr (BAL && !CULL) {
+#if PBR_BAL_PROFILE
+                BAL_PROF_ADD(7, (long long)__builtin_amdgcn_s_memtime() - t_entry);
+#endif
+                d2 = lighting_fast<false, true, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo,
+                                                            kept_total, &s.bal[wave_id], s.bal_light, ga, gb_);
+#if PBR_BAL_PROFILE
+                const long long t_l1 = (long long)__builtin_amdgcn_s_memtime();
+#endif
+                // The pair's 44 invariant registers are not kept live across the balanced loop (that spilled):
+                // reload the pair (L2-resident by now) from hardware-derived coordinates -- the same pixels as
+                // xa, y -- and rebuild the unscaled invariants with the same arithmetic (same bits).
+                const int ln = lane_id_fresh();
+                const int64_t r2 = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride +
+                                   blockIdx.x * kTileW + 2 * (ln & 31);
+#if PBR_BAL_EXPERIMENT == 2  // timing experiment: no reload (wrong frames)
+                p.pos = p.n = p.albedo = p.f0 = splat3(0.5f, 0.5f, 0.5f);
+                p.metallic = p.roughness = p.ao = splat(0.5f);
+                (void)r2;
+#else
+                p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? r2 : 0, vb ? r2 + 1 : 0, vb && gb.pairs_aligned);
+#endif
+                q2 = pair_invariants(p, ps, fast2);
+                pos2 = p.pos;
+                ao_a = p.ao.x;
+                ao_b = p.ao.y;
+#if PBR_BAL_PROFILE
+                const v2 dep = dot3(q2.n, q2.v);  // wait for the reload before stamping
+                if (dep.x == 12345.0f) ao_a = 0.5f;
+                BAL_PROF_ADD(8, (long long)__builtin_amdgcn_s_memtime() - t_l1);
+#endif
+            } else {
+                d2 = lighting_fast<CULL, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+                if (!CULL) faithful_unscale(q2);
+            }
         } else if (faithful_wave) {
             if (!CULL) faithful_scale(q2);
             d2 = lighting_fast<CULL, false, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
@@ -538,6 +597,9 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         const int n = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
         if (n != 0 && (tid & 63) == 0) atomicAdd(&s.exact_px, n);
     }
+#if PBR_BAL_PROFILE
+    const long long t_b0 = (long long)__builtin_amdgcn_s_memtime();
+#endif
     if (__syncthreads_or(need_a || need_b)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
         f3 ea, eb;
         lighting_exact<false>(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, s, TileBounds{},
@@ -552,6 +614,13 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         tile_kept[kStatsPerBlock * t + 2] = s.exact_px;
     }
 
+#if PBR_BAL_PROFILE
+    if constexpr (BAL) {
+        const long long t_b1 = (long long)__builtin_amdgcn_s_memtime();
+        BAL_PROF_ADD(6, t_b1 - t_entry);
+        BAL_PROF_ADD(9, t_b1 - t_b0);
+    }
+#endif
     // The output offset re-derived from the hardware ids (lane_id_fresh): same pixel as xa, y above.
     const int ln = lane_id_fresh();
     const int sx = blockIdx.x * kTileW + 2 * (ln & 31);
@@ -713,8 +782,12 @@ template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
     if (a.pixels_per_thread == 2) {
         dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
-        hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream, a.gb,
-                           a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
+        if (!CULL && a.ps.balanced)
+            hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, true>), grid, dim3(kBlock), 0,
+                               stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
+        else
+            hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,
+                               a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
     } else {
         dim3 grid((a.gb.width + kTileW1 - 1) / kTileW1, (a.gb.height + kTileH - 1) / kTileH);
         hipLaunchKernelGGL((shade_tile1_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,
@@ -746,6 +819,22 @@ hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream) {
 int64_t shade_tile_count(int width, int height, int pixels_per_thread) {
     const int tw = pixels_per_thread == 2 ? kTileW : kTileW1;
     return (int64_t)((width + tw - 1) / tw) * ((height + kTileH - 1) / kTileH);
+}
+
+// Development builds with PBR_BAL_PROFILE: read (and optionally clear) the balanced pass's clock sums.
+hipError_t debug_bal_profile(unsigned long long* out8, bool reset) {
+#if PBR_BAL_PROFILE
+    hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_bal_prof), sizeof(unsigned long long) * 16);
+    if (e == hipSuccess && reset) {
+        const unsigned long long z[16] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_bal_prof), z, sizeof(z));
+    }
+    return e;
+#else
+    (void)out8;
+    (void)reset;
+    return hipErrorNotSupported;
+#endif
 }
 
 hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream) {

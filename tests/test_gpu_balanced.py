@@ -1,0 +1,178 @@
+"""Wave-balanced point-light lists (pbr_balanced.h): back-face rejection + cross-lane rebalancing.
+
+The balanced kernel evaluates each live (pixel, light) item with the same operations as the packed faithful
+loop and skips only items whose reference term is +-0; it sums each pixel's live terms in two interleaved
+partial sums, so its frames differ from the unbalanced faithful kernel's by the association of the sum
+only: both must be within the north-star 1e-5 of the oracle, and within a few ulps of each other. The
+contexts here choose the path through PBR_BALANCED_MIN, which pbr_context_create reads (0 = never
+balanced, 1 = every untiled faithful pass with point lights only).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import oracle_pass_from_constants
+from oracle import oracle as O
+from physically_based_renderer_amd import _native as N
+from physically_based_renderer_amd import scenes as S
+from physically_based_renderer_amd.renderer import GBuffer, PassConstants, ShadingContext
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-5
+ASSOC_TOL = 64 * 2.0 ** -23  # <= 64 summed non-negative terms: re-association moves the sum by <= 1 ulp per term
+
+
+def close(a, b):
+    """Frames that differ only by the association of the light sum (NaN == NaN)."""
+    return O.rel_err(a, b).max() <= ASSOC_TOL
+
+
+@pytest.fixture(scope="module")
+def ctx_pair(gpu):
+    """(balanced, unbalanced) shading contexts."""
+    import os
+
+    old = os.environ.get("PBR_BALANCED_MIN")
+    os.environ["PBR_BALANCED_MIN"] = "1"
+    bal = ShadingContext(0)
+    os.environ["PBR_BALANCED_MIN"] = "0"
+    plain = ShadingContext(0)
+    if old is None:
+        del os.environ["PBR_BALANCED_MIN"]
+    else:
+        os.environ["PBR_BALANCED_MIN"] = old
+    yield bal, plain
+    bal.close()
+    plain.close()
+
+
+def faithful(pc):
+    return PassConstants(**{**pc.__dict__, "flags": pc.flags | N.PBR_FLAG_FAITHFUL})
+
+
+def run(ctx, gb, pc, env=None):
+    ctx.set_pass(pc)
+    if env is not None:
+        ctx.set_env_map(env)
+    out = ctx.shade(gb)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), ctx.pass_stats()["exact_pixels"]
+
+
+@pytest.mark.parametrize("cid,size", [(2, (1920, 256)), (3, (1024, 256)), (3, (1000, 77)), (1, None)])
+def test_balanced_equals_unbalanced_and_oracle(cid, size, ctx_pair, gpu, env_map):
+    """Scene configs (odd sizes included: partial waves and tiles): same frames up to the sum's association,
+    same redo sets."""
+    cfg = S.CONFIGS[cid] if size is None else S.CONFIGS[cid].with_size(*size)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = faithful(S.scene_pass(cfg))
+    env = env_map if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc, env)
+    want, redo_p = run(plain, gb, pc, env)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), env, n_threads=16)
+    e = O.rel_err(got, ref)
+    print(f"{cfg.name} {cfg.width}x{cfg.height}: balanced max_rel={e.max():.3g}, redo {redo_b} vs {redo_p}")
+    assert close(got, want)
+    assert redo_b == redo_p
+    assert e.max() <= REL_TOL
+
+
+def _scene(rng, w, h, n_lights):
+    n = w * h
+    pos = np.stack([rng.uniform(-10, 10, n), rng.uniform(-10, 10, n), rng.uniform(0, 10, n)], 1)
+    nrm = rng.normal(size=(n, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    planes = np.zeros((15, h, w), np.float32)
+    planes[0:3] = pos.T.reshape(3, h, w)
+    planes[3:6] = nrm.T.reshape(3, h, w)
+    planes[6:9] = rng.uniform(0, 1, (3, h, w))
+    planes[9] = rng.uniform(0, 1, (h, w))
+    planes[10] = rng.uniform(0, 1, (h, w))
+    planes[11] = 1.0
+    lights = np.zeros((n_lights, 12), np.float32)
+    lights[:, 0:3] = rng.uniform(0, 100, (n_lights, 3))
+    lights[:, 8:11] = np.stack([rng.uniform(-20, 20, n_lights), rng.uniform(-20, 20, n_lights),
+                                rng.uniform(-20, 0, n_lights)], 1)
+    return planes, lights
+
+
+def test_balanced_back_face_edges(ctx_pair, gpu):
+    """Items at the edges of the back-face test:
+    * L == -V exactly (eye, pixel and light collinear, pixel facing the eye): the reference's
+      H = normalize(V + L) is NaN, but max(dot(N, H), 0) and saturate(dot(H, V)) map it to 0 and with
+      N.L = -1 the term is +0, so the item is skipped (the unbalanced loop sends the pixel to the exact
+      re-pass instead, for its |V + L| window: same bits, different redo counts);
+    * the pixel on a light (l == 0: the reference's L = 0 / 0 is NaN, absorbed the same way; the item stays
+      live through the test's 2^-120 seed and the dist window sends the pixel to the exact re-pass);
+    * N.L within a few ulps of 0 (lights in the pixel's tangent plane, slightly behind / in front);
+    * a light beyond the 100-unit range behind the pixel, and lights 1e-3 behind it."""
+    rng = np.random.default_rng(7)
+    w, h, nl = 128, 4, 20
+    planes, lights = _scene(rng, w, h, nl)
+    eye = np.array([0.0, 0.0, -5.0], np.float32)
+    # row 0: pixels on the z axis facing the eye, a light straight behind each (L == -V exactly)
+    for x in range(0, 16):
+        z = np.float32(x * 0.5)
+        planes[0:3, 0, x] = (0.0, 0.0, z)
+        planes[3:6, 0, x] = (0.0, 0.0, -1.0)
+    lights[0, 8:11] = (0.0, 0.0, 20.0)
+    # row 1: pixels exactly on light 1 and on light 2
+    planes[0:3, 1, 0] = lights[1, 8:11]
+    planes[0:3, 1, 1] = lights[2, 8:11]
+    # row 2: tangent-plane lights: N = +y, light j at the pixel's height +- a few ulps
+    for x in range(0, 32):
+        p = np.array([x * 0.25 - 4.0, 1.0, 2.0], np.float32)
+        planes[0:3, 2, x] = p
+        planes[3:6, 2, x] = (0.0, 1.0, 0.0)
+    for j, dy in zip(range(3, 9), (0.0, 1e-7, -1e-7, 1e-6, -1e-6, 3e-5)):
+        lights[j, 8:11] = (5.0, np.float32(1.0) + np.float32(dy), 2.5)
+    # row 3: lights just behind (1e-3) and far behind (150) the pixel
+    planes[0:3, 3, 0] = (1.0, 1.0, 1.0)
+    planes[3:6, 3, 0] = (0.0, 0.0, -1.0)
+    lights[9, 8:11] = (1.0, 1.0, 1.001)
+    lights[10, 8:11] = (1.0, 1.0, 151.0)
+    pc = PassConstants(eye_pos_w=tuple(eye), num_point_lights=nl, lights_array=lights, flags=N.PBR_FLAG_FAITHFUL)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc)
+    want, redo_p = run(plain, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    print(f"edges: redo {redo_b} vs {redo_p}; NaN pixels {int(np.isnan(ref[..., 0]).sum())}")
+    assert np.isfinite(ref[0, :16]).all()  # the L == -V pixels: the NaN H is absorbed by maxNum
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert close(got, want)
+    assert redo_b <= redo_p
+    assert O.rel_err(got, ref).max() <= REL_TOL
+
+
+@pytest.mark.parametrize("n_lights", [1, 31, 32, 33, 63, 64])
+def test_balanced_light_counts(n_lights, ctx_pair, gpu):
+    """Mask-word boundaries (32 lights per word) and the one-light pass."""
+    rng = np.random.default_rng(100 + n_lights)
+    planes, lights = _scene(rng, 256, 8, n_lights)
+    pc = PassConstants(num_point_lights=n_lights, lights_array=lights, flags=N.PBR_FLAG_FAITHFUL)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, _ = run(bal, gb, pc)
+    want, _ = run(plain, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    assert close(got, want)
+    assert O.rel_err(got, ref).max() <= REL_TOL
+
+
+def test_balanced_light_outside_window_sends_all_to_exact(ctx_pair, gpu):
+    """A light whose position is outside the fast-path window (|x| > 2^20): every pixel is redone exactly,
+    as in the uniform loop (frames bit-identical to the oracle there)."""
+    rng = np.random.default_rng(5)
+    planes, lights = _scene(rng, 128, 4, 20)
+    lights[7, 8] = 3.0e6
+    pc = PassConstants(num_point_lights=20, lights_array=lights, flags=N.PBR_FLAG_FAITHFUL)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc)
+    want, redo_p = run(plain, gb, pc)
+    assert redo_b == redo_p == 128 * 4
+    assert close(got, want)

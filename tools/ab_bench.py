@@ -1,6 +1,6 @@
 """Same-box A/B timing of kernel builds (development tool; not part of the product or the tests).
 
-    python tools/ab_bench.py --libs A.so B.so [--configs 3 4 2] [--rounds 2] [--reps 30]
+    python tools/ab_bench.py --libs A.so B.so[@ENV=VALUE,...] [--configs 3 4 2] [--rounds 2] [--reps 30]
 
 Each (round, lib, config) runs in a fresh subprocess with PBR_LIB_PATH pointing at that build: the
 G-buffer is filled, the clock ramped (tools/clock_ramp.py), then `reps` launches are timed with HIP
@@ -18,6 +18,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def one(lib: str, cid: int, reps: int, flags: int = 0) -> dict:
+    label = lib
+    if "@" in lib:  # "build.so@NAME=VALUE,NAME=VALUE": environment for this leg (e.g. PBR_BALANCED_MIN=0)
+        lib, envs = lib.split("@", 1)
+        for kv in envs.split(","):
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
     os.environ["PBR_LIB_PATH"] = os.path.abspath(lib)
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -50,7 +56,7 @@ def one(lib: str, cid: int, reps: int, flags: int = 0) -> dict:
         ms = [a.elapsed_time(b) for a, b in ev]
         bits = out.view(torch.int32).to(torch.int64)
         csum = int((bits * (torch.arange(bits.numel(), device=dev, dtype=torch.int64).view(bits.shape) % 65521 + 1)).sum())
-    return {"lib": os.path.basename(lib), "config": cid, "median_ms": float(np.median(ms)), "min_ms": float(np.min(ms)),
+    return {"lib": os.path.basename(label), "config": cid, "median_ms": float(np.median(ms)), "min_ms": float(np.min(ms)),
             "mpix_s": cfg.width * cfg.height / float(np.median(ms)) / 1e3, "checksum": csum}
 
 

@@ -1,0 +1,66 @@
+"""Per-phase shader-clock breakdown of the wave-balanced point-light pass (development tool).
+
+Needs a library built with -DPBR_BAL_PROFILE=1 (make -C physically_based_renderer_amd/csrc EXTRA=...),
+passed as PBR_LIB_PATH. Shades config `--config` (faithful) `--reps` times and prints the average shader
+cycles per balanced wave in each phase, the pass-2 iterations per wave, and the whole kernel per wave.
+
+    PBR_LIB_PATH=build/ab/balprof.so python tools/bal_profile.py --config 3
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    import torch
+
+    from clock_ramp import clock_ramp
+    from physically_based_renderer_amd import _native as N
+    from physically_based_renderer_amd import scenes as S
+    from physically_based_renderer_amd.renderer import GBuffer, ShadingContext
+
+    cfg = S.CONFIGS[a.config]
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    pc.flags = int(pc.flags) | N.PBR_FLAG_FAITHFUL
+    dev = torch.device("cuda", 0)
+    gb = GBuffer.from_host(planes, dev)
+    out = torch.empty((cfg.height, cfg.width, 4), device=dev)
+    lib = N.lib()
+    f = lib.pbr_debug_bal_profile
+    f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    buf = (ctypes.c_ulonglong * 16)()
+    with ShadingContext(0) as ctx:
+        ctx.set_pass(pc)
+        if pc.ambient_mode:
+            ctx.set_env_map(S.env_map())
+        clock_ramp(ctx, gb, out)
+        torch.cuda.synchronize()
+        assert f(buf, 1) == 0, "library not built with PBR_BAL_PROFILE"
+        for _ in range(a.reps):
+            ctx.shade(gb, out)
+        torch.cuda.synchronize()
+        assert f(buf, 1) == 0
+    waves = max(buf[4], 1)
+    names = ["pass 1", "rank + exchange", "pass 2", "hand-back"]
+    print(f"{cfg.name}: {waves // a.reps} balanced waves per frame")
+    for i, nm in enumerate(names):
+        print(f"  {nm:16s} {buf[i] / waves:10.0f} cycles/wave")
+    print(f"  pass-2 iterations {buf[5] / waves:8.2f} per wave")
+    print(f"  whole kernel     {buf[6] / waves:10.0f} cycles/wave (entry to the exact re-pass barrier's end)")
+    print(f"  entry -> light loop      {buf[7] / waves:10.0f}")
+    print(f"  loop end -> reloaded inv {buf[8] / waves:10.0f}")
+    print(f"  exact re-pass barrier    {buf[9] / waves:10.0f}")
+
+
+if __name__ == "__main__":
+    main()
