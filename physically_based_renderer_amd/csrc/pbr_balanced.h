@@ -21,22 +21,24 @@
 // lights) added at the end: a different association than the reference's, inside the faithful bound
 // (non-negative terms).
 //
-// The back-face test (pass 1) for light j and pixel P, with l = Light.Position - P as the reference forms it:
-//   skip  <=>  t1 = N.l + c |N|_1 B_j < 0     (c = 2^-18, N.l by FMAs)
-// where B_j >= |l| for every pixel of the wave: the L1 distance from the light to the centre of the wave's
-// position box plus the box's L1 half-extent, with margins for their roundings (computed once per wave, one
-// lane per light). t1 < 0 bounds the reference's max(dot(N, L), 0) (L = l / length(l), HLSL dot) to 0: the
-// rounding error of N.l here is <= 3u sum|N_i l_i| and that of the reference's dot(N, L) <= ~9u |N|_1
-// (u = 2^-24), both far below c |N|_1 = 64u |N|_1 (N.l < -c |N|_1 B_j <= -c |N|_1 |l|). With N.L = 0 the reference's term is +-0 whatever H is: where
-// V + L = 0 its H = normalize(V + L) is NaN, but max(dot(N, H), 0) and saturate(dot(H, V)) map NaN to 0 (IEEE
-// maxNum, LightingUtil.hlsl:55, 45), so NDF and F stay finite and G = 0. Every other factor is finite for a
-// pixel and light inside the fast-path window (the lean-wave bounds of brdf_x2: den in [2^-37, PI], F0 window;
-// attenuation <= 1e4). l == 0 (pixel on the light: 0 / 0 in the reference) keeps the item live through the
-// 2^-120 seed of the N.l chain. So every skipped term is +-0 in the reference and needs no window test; live
-// items run the usual window tests (the plain loop also sends pixels with |V + L| < 2^-30 to the exact
-// re-pass; here that happens only when such an item is live). Lights whose fast-path flag is off
-// (pbr_set_pass) make the host choose the uniform loop (PassArgs::balanced), which sends every pixel to the
-// exact re-pass.
+// The back-face test (pass 1) for light j at p_j and pixel P (l = p_j - P, the reference's L before it is
+// normalised), four FMAs per pixel:
+//   skip  <=>  t1 = N.p_j - N.P + c |N|_1 B_j < 0     (c = 2^-18 = 64u, u = 2^-24; N.P once per pixel)
+// B_j = B0_j + (|p_j|_1 + Pmax) / 8 (times 1 + 2^-20), where B0_j >= |l| for every pixel of the wave (the
+// L1 distance from the light to the centre of the wave's position box plus the box's L1 half-extent, with
+// margins for their roundings) and Pmax is the wave's largest |P|_1; computed once per wave, one lane per
+// light. The FMA chain's error is <= 7u (c |N|_1 B_j + |N|_inf (|p_j|_1 + |P|_1)), and the second term of
+// B_j covers the second part (c / 8 = 8u > 7u), so t1 < 0 gives N.l < -c |N|_1 |l| (1 - 7u). That bounds the
+// reference's max(dot(N, L), 0) (L = l / length(l), HLSL dot; its rounding error is <= ~9u |N|_1) to 0.
+// With N.L = 0 the reference's term is +-0 whatever H is: where V + L = 0 its H = normalize(V + L) is NaN, but
+// max(dot(N, H), 0) and saturate(dot(H, V)) map NaN to 0 (IEEE maxNum, LightingUtil.hlsl:55, 45), so NDF and
+// F stay finite and G = 0. The pixel on the light (l = 0: L = 0 / 0 = NaN) is the same case. Every other
+// factor is finite for a pixel and light inside the fast-path window (the lean-wave bounds of brdf_x2: den in
+// [2^-37, PI], F0 window; attenuation <= 1e4). So every skipped term is +-0 in the reference and needs no
+// window test; live items run the usual window tests (the plain loop also sends pixels with |V + L| < 2^-30
+// or a light closer than 0.01 to the exact re-pass for such items; here that happens only when the item is
+// live). Lights whose fast-path flag is off (pbr_set_pass) make the host choose the uniform loop
+// (PassArgs::balanced), which sends every pixel to the exact re-pass.
 #pragma once
 #include <cstdint>
 
@@ -52,16 +54,22 @@ constexpr int kBalRec = 7;         // float4 per exchanged pixel record
 #ifndef PBR_BAL_EXPERIMENT
 #define PBR_BAL_EXPERIMENT 0  // development timing switches (0 = product)
 #endif
+#ifndef PBR_BAL_PIPELINE
+#define PBR_BAL_PIPELINE 0  // pass 2 reads the next pair's lights ahead (measured slower: 1.69 vs 1.01 ms)
+#endif
 #ifndef PBR_BAL_PROFILE
 #define PBR_BAL_PROFILE 0  // development build: per-phase shader-clock sums (pbr_debug_bal_profile)
 #endif
 #if PBR_BAL_PROFILE
 // [0] pass 1, [1] rank + exchange, [2] pass 2, [3] hand-back, [4] waves, [5] pass-2 iterations,
 // [6] whole kernel (entry to the stores), [7] entry to the light loop, [8] light loop end to the reloaded
-// invariants, [9] to after the exact re-pass barrier, [10] to the stores
-__device__ unsigned long long g_bal_prof[16];
+// invariants, [9] the exact re-pass barrier; the unbalanced kernel's faithful lean waves: [11] entry to the
+// light loop, [12] the light loop, [13] waves, [14] the barrier, [15] entry to after the barrier
+// Each wave sums its stamps in its own LDS slots (bal_prof, lane 0) and adds them to its own slots of
+// g_bal_prof_buf at the end (plain loads and stores: no contended atomics to perturb the timing).
+__device__ unsigned long long* g_bal_prof_buf;  // 16 per wave, wave = block * 4 + wave in block
 #define BAL_PROF_T(v) const long long v = (long long)__builtin_amdgcn_s_memtime()
-#define BAL_PROF_ADD(slot_, val_) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_bal_prof[slot_], (unsigned long long)(val_)); } while (0)
+#define BAL_PROF_ADD(slot_, val_) do { if ((threadIdx.x & 63) == 0) bal_prof[slot_] += (unsigned long long)(val_); } while (0)
 #else
 #define BAL_PROF_T(v)
 #define BAL_PROF_ADD(i, x)
@@ -173,13 +181,11 @@ __device__ __forceinline__ float bal_wave_max(float v) {
     return v;
 }
 
-// Pass 1 for the pair and one light (position lx, ly, lz, distance bound bj): shift the light's SKIP bit for
-// each pixel (the sign of t1, see the header comment) into `ma` / `mb` (bit 31 after this call).
+// Pass 1 for the pair and one light (position lx, ly, lz, bound bj): shift the light's SKIP bit for each pixel
+// (the sign of t1, see the header comment) into `ma` / `mb` (bit 31 after this call). nd = -N.P per pixel.
 __device__ __forceinline__ void push_skip_bits(uint32_t& ma, uint32_t& mb, float lx, float ly, float lz, float bj,
-                                               const f3x2& pos, const f3x2& n, v2 cn) {
-    const f3x2 l = f3x2{lx - pos.x, ly - pos.y, lz - pos.z};  // LightingUtil.hlsl:127
-    const v2 nl = vfma(n.z, l.z, vfma(n.y, l.y, vfma(n.x, l.x, splat(0x1p-120f))));
-    const v2 t1 = vfma(cn, splat(bj), nl);
+                                               const f3x2& n, v2 nd, v2 cn) {
+    const v2 t1 = vfma(n.x, splat(lx), vfma(n.y, splat(ly), vfma(n.z, splat(lz), vfma(cn, splat(bj), nd))));
     ma = __builtin_amdgcn_alignbit(ma, __float_as_uint(t1.x), 31);  // (m << 1) | sign(t1)
     mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(t1.y), 31);
 }
@@ -223,7 +229,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
                                                          const f3x2& pos, bool live_a, bool live_b,
                                                          const float4* __restrict__ lights, int b0, int b1,
                                                          BalancedWaveLds& w, const float* lds_lights, f3x2& sum,
-                                                         m2& redo) {
+                                                         m2& redo, unsigned long long* bal_prof = nullptr) {
     const int lane_id = (int)(threadIdx.x & 63);
     const int n = b1 - b0;
     BAL_PROF_T(t0);
@@ -242,33 +248,42 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     const float cx = 0.5f * mnx + 0.5f * mxx, cy = 0.5f * mny + 0.5f * mxy, cz = 0.5f * mnz + 0.5f * mxz;
     const float r = (0.5f * (mxx - mnx) + 0.5f * (mxy - mny)) + 0.5f * (mxz - mnz);
     const float slack = r + (fabsf(cx) + fabsf(cy) + fabsf(cz)) * 0x1p-22f;
+    const float pmax = bal_wave_max(fmaxf(live_a ? (fabsf(pa.x) + fabsf(pa.y)) + fabsf(pa.z) : 0.0f,
+                                          live_b ? (fabsf(pb.x) + fabsf(pb.y)) + fabsf(pb.z) : 0.0f));
     if (lane_id < kBalLdsStride - 4) {  // B_j for j < n; padded lights (zero position) get a bound too
         const float lx = lds_lights[lane_id], ly = lds_lights[kBalLdsStride + lane_id],
                     lz = lds_lights[2 * kBalLdsStride + lane_id];
-        reinterpret_cast<float*>(w.bound)[lane_id] =
-            (((fabsf(lx - cx) + fabsf(ly - cy)) + fabsf(lz - cz)) + slack) * (1.0f + 0x1p-20f);
+        const float b0 = ((fabsf(lx - cx) + fabsf(ly - cy)) + fabsf(lz - cz)) + slack;
+        const float far = ((fabsf(lx) + fabsf(ly)) + fabsf(lz)) + pmax;
+        reinterpret_cast<float*>(w.bound)[lane_id] = (b0 + 0.125f * far) * (1.0f + 0x1p-20f);
     }
     wave_lds_sync();
     const v2 cn = v2{0x1p-18f * ((fabsf(q.n.x.x) + fabsf(q.n.y.x)) + fabsf(q.n.z.x)),
                      0x1p-18f * ((fabsf(q.n.x.y) + fabsf(q.n.y.y)) + fabsf(q.n.z.y))};
+    const v2 nd = -vfma(q.n.z, pos.z, vfma(q.n.y, pos.y, q.n.x * pos.x));  // -N.P
     uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // skip bits; pixel a: a0 (lights 0..31), a1; pixel b: c0, c1
     // Four lights per step from uniform (broadcast) LDS reads, pushed from the highest light down so that
-    // light j ends at bit j % 32 of its word; the top step of a word may test padded lights (masked below).
+    // light j ends at bit j % 32 of its word. A word always runs all 32 of its lights (padded lights are zero
+    // records whose bits are masked below): straight-line code, in which the compiler issues the LDS reads of
+    // later steps ahead of the arithmetic of earlier ones -- the waves of a block run this phase nearly in
+    // step, so a read waited on at once would idle the SIMD for its latency.
     const float4* px4 = reinterpret_cast<const float4*>(lds_lights);
     const float4* py4 = reinterpret_cast<const float4*>(lds_lights + kBalLdsStride);
     const float4* pz4 = reinterpret_cast<const float4*>(lds_lights + 2 * kBalLdsStride);
-    auto word = [&](int lo, int hi, uint32_t& ma, uint32_t& mb) {  // lights [lo, hi), hi - lo <= 32
-        for (int q4 = (hi - 1) >> 2; q4 >= (lo >> 2); --q4) {
+    auto word = [&](int qbase, uint32_t& ma, uint32_t& mb) {  // lights [4 qbase, 4 qbase + 32)
+#pragma unroll
+        for (int k = 7; k >= 0; --k) {
+            const int q4 = qbase + k;
             const float4 x = px4[q4], y = py4[q4], z = pz4[q4], b = w.bound[q4];
-            push_skip_bits(ma, mb, x.w, y.w, z.w, b.w, pos, q.n, cn);
-            push_skip_bits(ma, mb, x.z, y.z, z.z, b.z, pos, q.n, cn);
-            push_skip_bits(ma, mb, x.y, y.y, z.y, b.y, pos, q.n, cn);
-            push_skip_bits(ma, mb, x.x, y.x, z.x, b.x, pos, q.n, cn);
+            push_skip_bits(ma, mb, x.w, y.w, z.w, b.w, q.n, nd, cn);
+            push_skip_bits(ma, mb, x.z, y.z, z.z, b.z, q.n, nd, cn);
+            push_skip_bits(ma, mb, x.y, y.y, z.y, b.y, q.n, nd, cn);
+            push_skip_bits(ma, mb, x.x, y.x, z.x, b.x, q.n, nd, cn);
         }
     };
     const int n0 = n < 32 ? n : 32;
-    if (n > 32) word(32, n, a1, c1);
-    word(0, n0, a0, c0);
+    if (n > 32) word(8, a1, c1);
+    word(0, a0, c0);
     // Live masks (light j at bit j % 32 of its word); bits above a word's light count are not lights.
     const int n1 = n - n0;
     const uint32_t k0 = n0 == 32 ? ~0u : (1u << n0) - 1u, k1 = n1 == 32 ? ~0u : (1u << n1) - 1u;
@@ -333,14 +348,68 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
         second = true;
     };
     if (m == 0) next_pixel();
+#if PBR_BAL_PROFILE
+    int iters = 0;
+#endif
 #if PBR_BAL_EXPERIMENT == 1  // timing experiment: no pass 2
     m = 0;
     if (!second) next_pixel();
     m = 0;
 #endif
+#if PBR_BAL_PIPELINE
+    // Software pipelined: the light records of a lane's next pair are read from LDS before the current pair's
+    // arithmetic (the waves run this loop nearly in step; a read waited on at once idles the SIMD).
+    const float* L = lds_lights;
+    constexpr int S = kBalLdsStride;
+    // The next pair of lights of the current pixel: j0 < j1; one light left -> j1 = j0 with the zero strength
+    // (s1 = kBalMaxLights): the second element then adds +0.
+    auto pop2 = [&](int& j0, int& j1, int& s1) {
+        j0 = __builtin_ctzll(m);
+        m &= m - 1;
+        const bool two = m != 0;
+        j1 = two ? __builtin_ctzll(m) : j0;
+        m &= two ? m - 1 : m;
+        s1 = two ? j1 : kBalMaxLights;
+    };
+    auto fetch = [&](int j0, int j1, int s1, f3x2& lp, f3x2& ls) {
+        lp = f3x2{v2{L[j0], L[j1]}, v2{L[S + j0], L[S + j1]}, v2{L[2 * S + j0], L[2 * S + j1]}};
+        ls = f3x2{v2{L[3 * S + j0], L[3 * S + s1]}, v2{L[4 * S + j0], L[4 * S + s1]}, v2{L[5 * S + j0], L[5 * S + s1]}};
+    };
+    bool has = m != 0;  // the lane has a current pair
+    f3x2 lp{}, ls{};
+    {
+        int j0 = 0, j1 = 0, s1 = kBalMaxLights;
+        if (has) pop2(j0, j1, s1);
+        fetch(j0, j1, s1, lp, ls);
+    }
+    while (__builtin_amdgcn_ballot_w64(has) != 0) {
 #if PBR_BAL_PROFILE
-    int iters = 0;
+        ++iters;
 #endif
+        if (has) {
+            const bool more = m != 0;
+            int k0 = 0, k1 = 0, t1 = kBalMaxLights;  // without a next pair: harmless reads of light 0
+            if (more) pop2(k0, k1, t1);
+            f3x2 np, ns;
+            fetch(k0, k1, t1, np, ns);
+            m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests; only this lane's bits are read
+            faithful_point_items2(cur, lp, ls, oki, acc);
+            ok = ok && on(oki.x) && on(oki.y);
+            lp = np;
+            ls = ns;
+            has = more;
+            if (!has && !second) {
+                next_pixel();
+                has = m != 0;
+                if (has) {
+                    int j0, j1, s1;
+                    pop2(j0, j1, s1);
+                    fetch(j0, j1, s1, lp, ls);
+                }
+            }
+        }
+    }
+#else
     while (true) {
         const bool active = m != 0;
         if (__builtin_amdgcn_ballot_w64(active) == 0) break;
@@ -365,6 +434,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
             if (m == 0 && !second) next_pixel();
         }
     }
+#endif
     BAL_PROF_T(t3);
     const f3 acc_second = mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
     const bool ok_second = ok;

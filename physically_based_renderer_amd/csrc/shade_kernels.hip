@@ -23,6 +23,7 @@
 
 #include <cstdint>
 #include <type_traits>
+#include <vector>
 
 #include "pbr_device_math.h"
 #include "pbr_device_math_x2.h"
@@ -71,6 +72,9 @@ struct Lds {
     };
     int wave_cnt[kBlock / 64];
     float bounds[kBlock / 64][6];
+#if PBR_BAL_PROFILE
+    unsigned long long prof[kBlock / 64][16];
+#endif
     int kept_sum, geo_waves;  // tiled-culling statistics of the block
     int exact_px;             // pixels of the block the exact path redid
 };
@@ -186,7 +190,8 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
                                               const float4* __restrict__ lights, const PassArgs& ps,
                                               const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total,
                                               BalancedWaveLds* bal = nullptr, const float* bal_lights = nullptr,
-                                              bool geo_a = false, bool geo_b = false) {
+                                              bool geo_a = false, bool geo_b = false,
+                                              unsigned long long* bal_prof = nullptr) {
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     Faithful2 fi{};
     if (FAITHFUL) fi = make_faithful<!CULL>(q);
@@ -239,7 +244,8 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     // BALANCED passes have no spot lights (host: PassArgs::balanced): nothing reads q or pos after the
     // balanced loop, so the caller can drop them across it.
     if (BALANCED)
-        lighting_balanced_points(q, fi, pos, geo_a, geo_b, lights, pt_begin, sp_begin, *bal, bal_lights, direct, redo);
+        lighting_balanced_points(q, fi, pos, geo_a, geo_b, lights, pt_begin, sp_begin, *bal, bal_lights, direct, redo,
+                                 bal_prof);
     else
         run_kind(std::false_type{}, pt_begin, sp_begin);
     if (!BALANCED && end > sp_begin) run_kind(std::true_type{}, sp_begin, end);
@@ -463,6 +469,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     __shared__ Lds s;
 #if PBR_BAL_PROFILE
     const long long t_entry = (long long)__builtin_amdgcn_s_memtime();
+    unsigned long long* bal_prof = s.prof[__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6];
+    if ((threadIdx.x & 63) < 16) bal_prof[threadIdx.x & 63] = 0;
 #endif
     load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
     if (threadIdx.x == 0) s.kept_sum = s.geo_waves = s.exact_px = 0;
@@ -547,7 +555,13 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 BAL_PROF_ADD(7, (long long)__builtin_amdgcn_s_memtime() - t_entry);
 #endif
                 d2 = lighting_fast<false, true, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo,
-                                                            kept_total, &s.bal[wave_id], s.bal_light, ga, gb_);
+                                                            kept_total, &s.bal[wave_id], s.bal_light, ga, gb_,
+#if PBR_BAL_PROFILE
+                                                            s.prof[wave_id]
+#else
+                                                            nullptr
+#endif
+                );
 #if PBR_BAL_PROFILE
                 const long long t_l1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
@@ -574,8 +588,18 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 BAL_PROF_ADD(8, (long long)__builtin_amdgcn_s_memtime() - t_l1);
 #endif
             } else {
+#if PBR_BAL_PROFILE
+                const long long t_u0 = (long long)__builtin_amdgcn_s_memtime();
+                BAL_PROF_ADD(11, t_u0 - t_entry);
+                BAL_PROF_ADD(13, 1);
+#endif
                 d2 = lighting_fast<CULL, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
                 if (!CULL) faithful_unscale(q2);
+#if PBR_BAL_PROFILE
+                const v2 dep = d2.x + d2.y;
+                if (dep.x == 12345.0f) ao_a = 0.5f;
+                BAL_PROF_ADD(12, (long long)__builtin_amdgcn_s_memtime() - t_u0);
+#endif
             }
         } else if (faithful_wave) {
             if (!CULL) faithful_scale(q2);
@@ -615,10 +639,15 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     }
 
 #if PBR_BAL_PROFILE
-    if constexpr (BAL) {
+    {
         const long long t_b1 = (long long)__builtin_amdgcn_s_memtime();
-        BAL_PROF_ADD(6, t_b1 - t_entry);
-        BAL_PROF_ADD(9, t_b1 - t_b0);
+        BAL_PROF_ADD(BAL ? 6 : 15, t_b1 - t_entry);
+        BAL_PROF_ADD(BAL ? 9 : 14, t_b1 - t_b0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int l = threadIdx.x & 63;
+        const int64_t wv = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
+        if (l < 16 && g_bal_prof_buf != nullptr && wv < (int64_t)(1 << 18)) g_bal_prof_buf[wv * 16 + l] += bal_prof[l];
     }
 #endif
     // The output offset re-derived from the hardware ids (lane_id_fresh): same pixel as xa, y above.
@@ -824,11 +853,22 @@ int64_t shade_tile_count(int width, int height, int pixels_per_thread) {
 // Development builds with PBR_BAL_PROFILE: read (and optionally clear) the balanced pass's clock sums.
 hipError_t debug_bal_profile(unsigned long long* out8, bool reset) {
 #if PBR_BAL_PROFILE
-    hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_bal_prof), sizeof(unsigned long long) * 16);
-    if (e == hipSuccess && reset) {
-        const unsigned long long z[16] = {};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_bal_prof), z, sizeof(z));
+    constexpr size_t kWaves = 1 << 18, kBytes = kWaves * 16 * sizeof(unsigned long long);
+    static unsigned long long* buf = nullptr;
+    hipError_t e = hipSuccess;
+    if (!buf) {
+        e = hipMalloc(&buf, kBytes);
+        if (e == hipSuccess) e = hipMemset(buf, 0, kBytes);
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_bal_prof_buf), &buf, sizeof(buf));
+        if (e == hipSuccess) e = hipDeviceSynchronize();
     }
+    std::vector<unsigned long long> h(kWaves * 16);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), buf, kBytes, hipMemcpyDeviceToHost);
+    for (int i = 0; i < 16; ++i) out8[i] = 0;
+    for (size_t w = 0; w < kWaves; ++w)
+        for (int i = 0; i < 16; ++i) out8[i] += h[w * 16 + i];
+    if (e == hipSuccess && reset) e = hipMemset(buf, 0, kBytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     return e;
 #else
     (void)out8;

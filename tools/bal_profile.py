@@ -50,6 +50,14 @@ def main():
             ctx.shade(gb, out)
         torch.cuda.synchronize()
         assert f(buf, 1) == 0
+    if buf[13]:  # the unbalanced kernel (PBR_BALANCED_MIN=0)
+        u = buf[13]
+        print(f"{cfg.name}: unbalanced faithful lean waves {u // a.reps} per frame")
+        print(f"  entry -> light loop      {buf[11] / u:10.0f} cycles/wave")
+        print(f"  light loop               {buf[12] / u:10.0f}")
+        print(f"  exact re-pass barrier    {buf[14] / u:10.0f}")
+        print(f"  entry -> barrier end     {buf[15] / u:10.0f}")
+        return
     waves = max(buf[4], 1)
     names = ["pass 1", "rank + exchange", "pass 2", "hand-back"]
     print(f"{cfg.name}: {waves // a.reps} balanced waves per frame")
