@@ -224,14 +224,18 @@ __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const 
 // pixels take part (geometry). Adds each pixel's point-light sum into `sum` (any order is within the faithful
 // bound) and ORs the pixels that left the fast-path window into `redo`. Wave-uniform control
 // flow; no block barrier.
-// `lds_lights`: the pass's point lights [b0, b1) staged by the block (stage_balanced_lights).
-__device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2& q, const Faithful2& fi,
-                                                         const f3x2& pos, bool live_a, bool live_b,
-                                                         const float4* __restrict__ lights, int b0, int b1,
-                                                         BalancedWaveLds& w, const float* lds_lights, f3x2& sum,
-                                                         m2& redo, unsigned long long* bal_prof = nullptr) {
+// The live-light masks of the pair's pixels (pass 1), light j at bit j % 32 of word j / 32.
+struct BalMasks {
+    uint32_t a0, a1, c0, c1;  // pixel a: lights [0, 32), [32, 64); pixel b: the same
+};
+
+// Pass 1 for point lights [0, nl) of the pass (staged in `lds_lights`), from the pair's raw G-buffer position
+// and normal (the test is invariant under scaling N): run before the loop invariants exist, so that the two
+// never hold registers at the same time. Wave-uniform control flow.
+__device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& n, bool live_a, bool live_b, int nl,
+                                                   BalancedWaveLds& w, const float* lds_lights,
+                                                   unsigned long long* bal_prof = nullptr) {
     const int lane_id = (int)(threadIdx.x & 63);
-    const int n = b1 - b0;
     BAL_PROF_T(t0);
     // ---- pass 1: live masks of both pixels
     // The wave's position box (geometry pixels) -> centre c and L1 half-extent r; lane k computes light k's
@@ -258,9 +262,9 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
         reinterpret_cast<float*>(w.bound)[lane_id] = (b0 + 0.125f * far) * (1.0f + 0x1p-20f);
     }
     wave_lds_sync();
-    const v2 cn = v2{0x1p-18f * ((fabsf(q.n.x.x) + fabsf(q.n.y.x)) + fabsf(q.n.z.x)),
-                     0x1p-18f * ((fabsf(q.n.x.y) + fabsf(q.n.y.y)) + fabsf(q.n.z.y))};
-    const v2 nd = -vfma(q.n.z, pos.z, vfma(q.n.y, pos.y, q.n.x * pos.x));  // -N.P
+    const v2 cn = v2{0x1p-18f * ((fabsf(n.x.x) + fabsf(n.y.x)) + fabsf(n.z.x)),
+                     0x1p-18f * ((fabsf(n.x.y) + fabsf(n.y.y)) + fabsf(n.z.y))};
+    const v2 nd = -vfma(n.z, pos.z, vfma(n.y, pos.y, n.x * pos.x));  // -N.P
     uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // skip bits; pixel a: a0 (lights 0..31), a1; pixel b: c0, c1
     // Four lights per step from uniform (broadcast) LDS reads, pushed from the highest light down so that
     // light j ends at bit j % 32 of its word. A word always runs all 32 of its lights (padded lights are zero
@@ -271,27 +275,40 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     const float4* py4 = reinterpret_cast<const float4*>(lds_lights + kBalLdsStride);
     const float4* pz4 = reinterpret_cast<const float4*>(lds_lights + 2 * kBalLdsStride);
     auto word = [&](int qbase, uint32_t& ma, uint32_t& mb) {  // lights [4 qbase, 4 qbase + 32)
-#pragma unroll
+#pragma unroll 2
         for (int k = 7; k >= 0; --k) {
             const int q4 = qbase + k;
             const float4 x = px4[q4], y = py4[q4], z = pz4[q4], b = w.bound[q4];
-            push_skip_bits(ma, mb, x.w, y.w, z.w, b.w, q.n, nd, cn);
-            push_skip_bits(ma, mb, x.z, y.z, z.z, b.z, q.n, nd, cn);
-            push_skip_bits(ma, mb, x.y, y.y, z.y, b.y, q.n, nd, cn);
-            push_skip_bits(ma, mb, x.x, y.x, z.x, b.x, q.n, nd, cn);
+            push_skip_bits(ma, mb, x.w, y.w, z.w, b.w, n, nd, cn);
+            push_skip_bits(ma, mb, x.z, y.z, z.z, b.z, n, nd, cn);
+            push_skip_bits(ma, mb, x.y, y.y, z.y, b.y, n, nd, cn);
+            push_skip_bits(ma, mb, x.x, y.x, z.x, b.x, n, nd, cn);
         }
     };
-    const int n0 = n < 32 ? n : 32;
-    if (n > 32) word(8, a1, c1);
+    const int n0 = nl < 32 ? nl : 32;
+    if (nl > 32) word(8, a1, c1);
     word(0, a0, c0);
     // Live masks (light j at bit j % 32 of its word); bits above a word's light count are not lights.
-    const int n1 = n - n0;
+    const int n1 = nl - n0;
     const uint32_t k0 = n0 == 32 ? ~0u : (1u << n0) - 1u, k1 = n1 == 32 ? ~0u : (1u << n1) - 1u;
     a0 = live_a ? ~a0 & k0 : 0u;
     c0 = live_b ? ~c0 & k0 : 0u;
     a1 = live_a ? ~a1 & k1 : 0u;
     c1 = live_b ? ~c1 & k1 : 0u;
 
+    BAL_PROF_T(t1);
+    BAL_PROF_ADD(0, t1 - t0);
+    return BalMasks{a0, a1, c0, c1};
+}
+
+// `lds_lights`: the pass's point lights [b0, b1) staged by the block (stage_balanced_lights); `bm`: their live
+// masks from balanced_pass1.
+__device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2& q, const Faithful2& fi,
+                                                         const f3x2& pos, bool live_a, bool live_b, BalMasks bm,
+                                                         BalancedWaveLds& w, const float* lds_lights, f3x2& sum,
+                                                         m2& redo, unsigned long long* bal_prof = nullptr) {
+    const int lane_id = (int)(threadIdx.x & 63);
+    const uint32_t a0 = bm.a0, a1 = bm.a1, c0 = bm.c0, c1 = bm.c1;
     BAL_PROF_T(t1);
     // ---- rank the wave's 128 pixels by live count (counting sort; ties in LDS-atomic order, which only
     // decides which lane evaluates a pixel, never how)
@@ -452,7 +469,6 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     redo |= mask2(live_a && ra.w == 0.0f, live_b && rb.w == 0.0f);
 #if PBR_BAL_PROFILE
     BAL_PROF_T(t4);
-    BAL_PROF_ADD(0, t1 - t0);
     BAL_PROF_ADD(1, t2 - t1);
     BAL_PROF_ADD(2, t3 - t2);
     BAL_PROF_ADD(3, t4 - t3);

@@ -190,7 +190,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
                                               const float4* __restrict__ lights, const PassArgs& ps,
                                               const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total,
                                               BalancedWaveLds* bal = nullptr, const float* bal_lights = nullptr,
-                                              bool geo_a = false, bool geo_b = false,
+                                              bool geo_a = false, bool geo_b = false, BalMasks bm = BalMasks{},
                                               unsigned long long* bal_prof = nullptr) {
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     Faithful2 fi{};
@@ -244,8 +244,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     // BALANCED passes have no spot lights (host: PassArgs::balanced): nothing reads q or pos after the
     // balanced loop, so the caller can drop them across it.
     if (BALANCED)
-        lighting_balanced_points(q, fi, pos, geo_a, geo_b, lights, pt_begin, sp_begin, *bal, bal_lights, direct, redo,
-                                 bal_prof);
+        lighting_balanced_points(q, fi, pos, geo_a, geo_b, bm, *bal, bal_lights, direct, redo, bal_prof);
     else
         run_kind(std::false_type{}, pt_begin, sp_begin);
     if (!BALANCED && end > sp_begin) run_kind(std::true_type{}, sp_begin, end);
@@ -350,6 +349,24 @@ __device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArg
                     ps.fresnel_r0[2] + p.metallic * (p.albedo.z - ps.fresnel_r0[2])};
     }
     return p;
+}
+
+// An optimisation barrier on the pair's raw values: the compiler must assume they changed, so a computation
+// from them after this point is not merged with the same computation before it. No instructions.
+__device__ __forceinline__ void launder(v2& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void launder(f3x2& x) {
+    launder(x.x);
+    launder(x.y);
+    launder(x.z);
+}
+__device__ __forceinline__ void launder(PairIn& p) {
+    launder(p.pos);
+    launder(p.n);
+    launder(p.albedo);
+    launder(p.f0);
+    launder(p.metallic);
+    launder(p.roughness);
+    launder(p.ao);
 }
 
 // V = normalize(g_CameraPosW - pin.PosW) (Default.hlsl:53) and the BRDF invariants of the pair. In the window
@@ -553,37 +570,29 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             if constexpr (BAL && !CULL) {
 #if PBR_BAL_PROFILE
                 BAL_PROF_ADD(7, (long long)__builtin_amdgcn_s_memtime() - t_entry);
-#endif
-                d2 = lighting_fast<false, true, true, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo,
-                                                            kept_total, &s.bal[wave_id], s.bal_light, ga, gb_,
-#if PBR_BAL_PROFILE
-                                                            s.prof[wave_id]
+                unsigned long long* prof = s.prof[wave_id];
 #else
-                                                            nullptr
+                unsigned long long* prof = nullptr;
 #endif
-                );
+                // Pass 1 on the raw pair; then the scaled invariants for the loop, rebuilt from the raw pair (the
+                // q2 above is not used on this path, so it is not live across pass 1); after the loop the
+                // unscaled ones once more for the finish. launder() keeps the compiler from merging the
+                // rebuilds with the computation above (which would keep q2 live across the loop: it spilled).
+                const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, s.bal[wave_id], s.bal_light, prof);
+                launder(p);
+                q2 = pair_invariants(p, ps, fast2);
+                faithful_scale(q2);
+                d2 = lighting_fast<false, true, true, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
+                                                            kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
+                                                            prof);
 #if PBR_BAL_PROFILE
                 const long long t_l1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-                // The pair's 44 invariant registers are not kept live across the balanced loop (that spilled):
-                // reload the pair (L2-resident by now) from hardware-derived coordinates -- the same pixels as
-                // xa, y -- and rebuild the unscaled invariants with the same arithmetic (same bits).
-                const int ln = lane_id_fresh();
-                const int64_t r2 = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride +
-                                   blockIdx.x * kTileW + 2 * (ln & 31);
-#if PBR_BAL_EXPERIMENT == 2  // timing experiment: no reload (wrong frames)
-                p.pos = p.n = p.albedo = p.f0 = splat3(0.5f, 0.5f, 0.5f);
-                p.metallic = p.roughness = p.ao = splat(0.5f);
-                (void)r2;
-#else
-                p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? r2 : 0, vb ? r2 + 1 : 0, vb && gb.pairs_aligned);
-#endif
+                launder(p);
                 q2 = pair_invariants(p, ps, fast2);
                 pos2 = p.pos;
-                ao_a = p.ao.x;
-                ao_b = p.ao.y;
 #if PBR_BAL_PROFILE
-                const v2 dep = dot3(q2.n, q2.v);  // wait for the reload before stamping
+                const v2 dep = dot3(q2.n, q2.v);
                 if (dep.x == 12345.0f) ao_a = 0.5f;
                 BAL_PROF_ADD(8, (long long)__builtin_amdgcn_s_memtime() - t_l1);
 #endif
