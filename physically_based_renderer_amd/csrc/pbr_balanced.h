@@ -190,6 +190,39 @@ __device__ __forceinline__ void push_skip_bits(uint32_t& ma, uint32_t& mb, float
     mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(t1.y), 31);
 }
 
+// Pass 2's light records for one iteration (element 0: light j0; element 1: light j1 with the strength of
+// light s1) from the SoA staging: all twelve LDS reads issued back to back and one wait. Left to itself the
+// compiler interleaved reads and waits (three or four round trips per iteration), and the waves run this loop
+// nearly in step, so each round trip idled the SIMD.
+__device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0, int j1, int s1, f3x2& lp,
+                                                 f3x2& ls) {
+    typedef __attribute__((address_space(3))) const float lds_float;
+    const uint32_t base = (uint32_t)(uintptr_t)(const lds_float*)lds_lights;
+    const uint32_t a0 = base + 4u * (uint32_t)j0, a1 = base + 4u * (uint32_t)j1, b1 = base + 4u * (uint32_t)s1;
+    float x0, x1, y0, y1, z0, z1, r0, r1, g0, g1, u0, u1;
+    static_assert(kBalLdsStride * 4 == 272, "offsets below");
+    asm volatile(
+        "ds_read_b32 %0, %12\n\t"
+        "ds_read_b32 %1, %13\n\t"
+        "ds_read_b32 %2, %12 offset:272\n\t"
+        "ds_read_b32 %3, %13 offset:272\n\t"
+        "ds_read_b32 %4, %12 offset:544\n\t"
+        "ds_read_b32 %5, %13 offset:544\n\t"
+        "ds_read_b32 %6, %12 offset:816\n\t"
+        "ds_read_b32 %7, %14 offset:816\n\t"
+        "ds_read_b32 %8, %12 offset:1088\n\t"
+        "ds_read_b32 %9, %14 offset:1088\n\t"
+        "ds_read_b32 %10, %12 offset:1360\n\t"
+        "ds_read_b32 %11, %14 offset:1360\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(x1), "=&v"(y0), "=&v"(y1), "=&v"(z0), "=&v"(z1), "=&v"(r0), "=&v"(r1), "=&v"(g0),
+          "=&v"(g1), "=&v"(u0), "=&v"(u1)
+        : "v"(a0), "v"(a1), "v"(b1)
+        : "memory");
+    lp = f3x2{v2{x0, x1}, v2{y0, y1}, v2{z0, z1}};
+    ls = f3x2{v2{r0, r1}, v2{g0, g1}, v2{u0, u1}};
+}
+
 // ---- pass 2: two (pixel, light) items of the faithful scaled lean loop, packed ---------------------------
 // ComputePointLight (LightingUtil.hlsl:124-142) + BRDFCookTorrance for ONE pixel (q, splat into both elements)
 // and TWO lights (element e: position lp.*[e], strength ls.*[e]), added into `sum`: the operations of
@@ -271,18 +304,36 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
     // records whose bits are masked below): straight-line code, in which the compiler issues the LDS reads of
     // later steps ahead of the arithmetic of earlier ones -- the waves of a block run this phase nearly in
     // step, so a read waited on at once would idle the SIMD for its latency.
-    const float4* px4 = reinterpret_cast<const float4*>(lds_lights);
-    const float4* py4 = reinterpret_cast<const float4*>(lds_lights + kBalLdsStride);
-    const float4* pz4 = reinterpret_cast<const float4*>(lds_lights + 2 * kBalLdsStride);
+    // Two steps (eight lights) per LDS round trip: their sixteen 16-byte reads are issued back to back and
+    // waited on once (inline asm; left to itself the compiler waited after every few reads).
+    typedef __attribute__((address_space(3))) const float lds_float;
+    const uint32_t lbase = (uint32_t)(uintptr_t)(const lds_float*)lds_lights;
+    const uint32_t bbase = (uint32_t)(uintptr_t)(const lds_float*)reinterpret_cast<const float*>(w.bound);
     auto word = [&](int qbase, uint32_t& ma, uint32_t& mb) {  // lights [4 qbase, 4 qbase + 32)
-#pragma unroll 2
-        for (int k = 7; k >= 0; --k) {
-            const int q4 = qbase + k;
-            const float4 x = px4[q4], y = py4[q4], z = pz4[q4], b = w.bound[q4];
-            push_skip_bits(ma, mb, x.w, y.w, z.w, b.w, n, nd, cn);
-            push_skip_bits(ma, mb, x.z, y.z, z.z, b.z, n, nd, cn);
-            push_skip_bits(ma, mb, x.y, y.y, z.y, b.y, n, nd, cn);
-            push_skip_bits(ma, mb, x.x, y.x, z.x, b.x, n, nd, cn);
+        for (int k = 6; k >= 0; k -= 2) {  // steps k + 1 and k
+            const uint32_t la = lbase + 16u * (uint32_t)(qbase + k), ba = bbase + 16u * (uint32_t)(qbase + k);
+            float4 x1, y1, z1, b1, x0, y0, z0, b0;  // step k + 1 (lights 4(q + k) + 4..7), step k (+ 0..3)
+            asm volatile(
+                "ds_read_b128 %0, %8 offset:16\n\t"
+                "ds_read_b128 %1, %8 offset:288\n\t"
+                "ds_read_b128 %2, %8 offset:560\n\t"
+                "ds_read_b128 %3, %9 offset:16\n\t"
+                "ds_read_b128 %4, %8\n\t"
+                "ds_read_b128 %5, %8 offset:272\n\t"
+                "ds_read_b128 %6, %8 offset:544\n\t"
+                "ds_read_b128 %7, %9\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(x1), "=&v"(y1), "=&v"(z1), "=&v"(b1), "=&v"(x0), "=&v"(y0), "=&v"(z0), "=&v"(b0)
+                : "v"(la), "v"(ba)
+                : "memory");
+            push_skip_bits(ma, mb, x1.w, y1.w, z1.w, b1.w, n, nd, cn);
+            push_skip_bits(ma, mb, x1.z, y1.z, z1.z, b1.z, n, nd, cn);
+            push_skip_bits(ma, mb, x1.y, y1.y, z1.y, b1.y, n, nd, cn);
+            push_skip_bits(ma, mb, x1.x, y1.x, z1.x, b1.x, n, nd, cn);
+            push_skip_bits(ma, mb, x0.w, y0.w, z0.w, b0.w, n, nd, cn);
+            push_skip_bits(ma, mb, x0.z, y0.z, z0.z, b0.z, n, nd, cn);
+            push_skip_bits(ma, mb, x0.y, y0.y, z0.y, b0.y, n, nd, cn);
+            push_skip_bits(ma, mb, x0.x, y0.x, z0.x, b0.x, n, nd, cn);
         }
     };
     const int n0 = nl < 32 ? nl : 32;
@@ -441,12 +492,9 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
             m &= two ? m - 1 : m;
             const int s1 = two ? j1 : kBalMaxLights;         // ... with the zero strength: it adds +0
             m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests; only this lane's bits are read
-            const float* L = lds_lights;
-            constexpr int S = kBalLdsStride;
-            faithful_point_items2(cur, f3x2{v2{L[j0], L[j1]}, v2{L[S + j0], L[S + j1]}, v2{L[2 * S + j0], L[2 * S + j1]}},
-                                  f3x2{v2{L[3 * S + j0], L[3 * S + s1]}, v2{L[4 * S + j0], L[4 * S + s1]},
-                                       v2{L[5 * S + j0], L[5 * S + s1]}},
-                                  oki, acc);
+            f3x2 lp, ls;
+            read_pair_lights(lds_lights, j0, j1, s1, lp, ls);
+            faithful_point_items2(cur, lp, ls, oki, acc);
             ok = ok && on(oki.x) && on(oki.y);
             if (m == 0 && !second) next_pixel();
         }
