@@ -41,12 +41,14 @@ struct pbr_context {
     bool pass_set = false;
     bool faithful_pass_ok = false;  // light strengths and the constant ambient are finite and >= 0
     bool faithful_count_terms = false;  // > 64 lights (culled pass): the kernel counts summed terms per wave
-    // Statistics of the last pass: one record of pbr::kStatsPerBlock int32 per workgroup ([surviving
+    // Statistics of the last pass: one record of pbr::kStatsPerBlock int32 per statistics slot (one per wave
+    // in the pair layout, per workgroup in the one-pixel layout; [surviving
     // point/spot lights summed over its culling tiles, culling tiles with geometry, pixels redone by the
     // exact path]), summed on the host by pbr_last_pass_stats / pbr_last_cull_stats.
     int32_t* d_tile_kept = nullptr;
     int64_t tile_kept_capacity = 0;
     int64_t last_tiles = 0;
+    int64_t last_slots = 0;  // statistics records of the last pass (shade_stat_slots_per_tile per tile)
     bool last_culled = false;
     // Wave-balanced point-light lists (pbr_balanced.h) for untiled faithful passes with at least this many
     // point lights and no spot lights; PBR_BALANCED_MIN overrides (0 disables).
@@ -373,7 +375,8 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     hipError_t e;
     {
         const int64_t tiles = pbr::shade_tile_count(gb->width, gb->height, a.pixels_per_thread);
-        if (tiles > ctx->tile_kept_capacity) {
+        const int64_t slots = tiles * pbr::shade_stat_slots_per_tile(a.pixels_per_thread);
+        if (slots > ctx->tile_kept_capacity) {
             // Growing: the old buffer may still be written by queued kernels on any stream.
             if (ctx->d_tile_kept) {
                 e = hipDeviceSynchronize();
@@ -382,11 +385,12 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
                 ctx->d_tile_kept = nullptr;
                 ctx->tile_kept_capacity = 0;
             }
-            e = hipMalloc(&ctx->d_tile_kept, pbr::kStatsPerBlock * sizeof(int32_t) * (size_t)tiles);
+            e = hipMalloc(&ctx->d_tile_kept, pbr::kStatsPerBlock * sizeof(int32_t) * (size_t)slots);
             if (e != hipSuccess) return fail_hip(ctx, e, "pass stats hipMalloc");
-            ctx->tile_kept_capacity = tiles;
+            ctx->tile_kept_capacity = slots;
         }
         ctx->last_tiles = tiles;
+        ctx->last_slots = slots;
         ctx->last_culled = cull;
         a.tile_kept = ctx->d_tile_kept;
     }
@@ -443,7 +447,7 @@ int sum_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream, const ch
     if (!g.ok) return PBR_ERR_NO_DEVICE;
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (ctx->last_tiles == 0) return PBR_OK;  // no pass yet (or an empty frame)
-    std::vector<int32_t> h(pbr::kStatsPerBlock * (size_t)ctx->last_tiles);
+    std::vector<int32_t> h(pbr::kStatsPerBlock * (size_t)ctx->last_slots);
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e = hipMemcpyAsync(h.data(), ctx->d_tile_kept, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -55,11 +55,12 @@ struct LaunchArgs {
     const float4* lights;  // 3 float4 per light (the reference's 48-byte Light)
     const float4* env;     // env_w * env_h RGBA fp32, or nullptr
     FrameArgs frame;
-    // kStatsPerBlock ints per workgroup (blockIdx.y * gridDim.x + blockIdx.x): surviving point/spot
-    // lights summed over its culling units and the number of culling units with geometry (both 0
-    // without CULL; the pair layout culls per wave = 64x2 pixels, the one-pixel layout per workgroup =
-    // 32x8), and the geometry pixels the exact path redid. Plain stores: one same-address global atomic
-    // per tile serialised the whole grid (0.29 ms per 4K frame). May be nullptr.
+    // kStatsPerBlock ints per statistics slot (shade_stat_slots_per_tile slots per workgroup, workgroup =
+    // blockIdx.y * gridDim.x + blockIdx.x): surviving point/spot lights summed over its culling units and the
+    // number of culling units with geometry (both 0 without CULL; the pair layout culls per wave = 64x2
+    // pixels and keeps one slot per wave, the one-pixel layout culls per workgroup = 32x8), and the geometry
+    // pixels the exact path redid. Plain stores: one same-address global atomic per tile serialised the
+    // whole grid (0.29 ms per 4K frame). May be nullptr.
     int32_t* tile_kept;
     int ambient_mode;
     bool f0_plane, apply_ao, cull;
@@ -70,6 +71,8 @@ struct LaunchArgs {
 hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);
 // Number of tiles (workgroups) launch_shade uses for a width x height G-buffer.
 int64_t shade_tile_count(int width, int height, int pixels_per_thread);
+// Statistics records per tile: one per wave in the pair layout, one per workgroup in the one-pixel layout.
+int shade_stat_slots_per_tile(int pixels_per_thread);
 hipError_t debug_bal_profile(unsigned long long* out8, bool reset);  // PBR_BAL_PROFILE builds only
 hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream);
 

@@ -310,6 +310,39 @@ __device__ __forceinline__ void lighting_exact(const PixelInvariants& qa, const 
     }
 }
 
+// The exact re-pass of the pair kernel, per wave: the same per-light functions as lighting_exact (the
+// compiler's IEEE sequences, reference order) with the light records read through the scalar cache instead of
+// staged in LDS, so that no block barrier is needed -- a wave whose lanes need no re-pass never waits for the
+// other waves of its block (the barrier cost ~4% of a wave's life in the balanced kernel). Wave-uniform.
+__device__ __forceinline__ void lighting_exact_wave(const PixelInvariants& qa, const PixelInvariants& qb, f3 pa,
+                                                    f3 pb, bool need_a, bool need_b, const float4* __restrict__ lights,
+                                                    const PassArgs& ps, f3& da, f3& db) {
+    da = mk3(0.0f, 0.0f, 0.0f);
+    db = mk3(0.0f, 0.0f, 0.0f);
+    bool unused = true;
+    for (int j = 0; j < ps.n_dir; ++j) {
+        const LightRec r = light_rec(lights, j);
+        if (need_a) da = add3(da, directional_light<false>(qa, r.s, r.d, unused));
+        if (need_b) db = add3(db, directional_light<false>(qb, r.s, r.d, unused));
+    }
+    const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
+    for (int j = pt_begin; j < end; ++j) {
+        const LightRec r = light_rec(lights, j);
+        const bool spot = j >= sp_begin;
+        f3 c;
+        if (need_a) {
+            const bool lit = spot ? point_or_spot_light<true, false>(qa, pa, r.s, r.d, r.p, c, unused)
+                                  : point_or_spot_light<false, false>(qa, pa, r.s, r.d, r.p, c, unused);
+            if (lit) da = add3(da, c);
+        }
+        if (need_b) {
+            const bool lit = spot ? point_or_spot_light<true, false>(qb, pb, r.s, r.d, r.p, c, unused)
+                                  : point_or_spot_light<false, false>(qb, pb, r.s, r.d, r.p, c, unused);
+            if (lit) db = add3(db, c);
+        }
+    }
+}
+
 // The pair's G-buffer values in packed form: element 0 = pixel A, element 1 = pixel B.
 struct PairIn {
     f3x2 pos, n, albedo, f0;
@@ -490,7 +523,6 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     if ((threadIdx.x & 63) < 16) bal_prof[threadIdx.x & 63] = 0;
 #endif
     load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
-    if (threadIdx.x == 0) s.kept_sum = s.geo_waves = s.exact_px = 0;
     if constexpr (BAL) stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light);
     __syncthreads();
 
@@ -618,33 +650,27 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
         else
             d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
-        if (CULL && (tid & 63) == 0) {  // per-tile statistics: survivors summed over the block's waves
-            atomicAdd(&s.kept_sum, kept_total);
-            atomicAdd(&s.geo_waves, 1);
-        }
     }
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
     f3 da = lane(d2, 0), db = lane(d2, 1);
     const bool need_a = ga && on(redo.x), need_b = gb_ && on(redo.y);
-    {  // statistics: pixels this wave sends to the exact path (scalar popcounts; LDS add only if any)
-        const int n = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
-        if (n != 0 && (tid & 63) == 0) atomicAdd(&s.exact_px, n);
+    // Statistics, one record per wave (kStatsPerBlock ints at slot tile * 4 + wave): culling survivors and
+    // whether the wave has geometry (culled passes), and the pixels it sends to the exact path.
+    const int n_exact = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
+    if ((tid & 63) == 0 && tile_kept != nullptr) {
+        const int64_t slot = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
+        tile_kept[kStatsPerBlock * slot] = CULL && wave_geometry ? kept_total : 0;
+        tile_kept[kStatsPerBlock * slot + 1] = CULL && wave_geometry ? 1 : 0;
+        tile_kept[kStatsPerBlock * slot + 2] = n_exact;
     }
 #if PBR_BAL_PROFILE
     const long long t_b0 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-    if (__syncthreads_or(need_a || need_b)) {  // block-uniform: rare (edge inputs, EXACT_ONLY)
+    if (n_exact != 0) {  // wave-uniform: rare (edge inputs, EXACT_ONLY)
         f3 ea, eb;
-        lighting_exact<false>(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, s, TileBounds{},
-                              false, ea, eb);
+        lighting_exact_wave(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, ea, eb);
         if (need_a) da = ea;
         if (need_b) db = eb;
-    }
-    if (tid == 0 && tile_kept != nullptr) {  // after the barrier above: every wave has added
-        const int64_t t = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-        tile_kept[kStatsPerBlock * t] = CULL ? s.kept_sum : 0;
-        tile_kept[kStatsPerBlock * t + 1] = CULL ? s.geo_waves : 0;
-        tile_kept[kStatsPerBlock * t + 2] = s.exact_px;
     }
 
 #if PBR_BAL_PROFILE
@@ -858,6 +884,8 @@ int64_t shade_tile_count(int width, int height, int pixels_per_thread) {
     const int tw = pixels_per_thread == 2 ? kTileW : kTileW1;
     return (int64_t)((width + tw - 1) / tw) * ((height + kTileH - 1) / kTileH);
 }
+
+int shade_stat_slots_per_tile(int pixels_per_thread) { return pixels_per_thread == 2 ? kBlock / 64 : 1; }
 
 // Development builds with PBR_BAL_PROFILE: read (and optionally clear) the balanced pass's clock sums.
 hipError_t debug_bal_profile(unsigned long long* out8, bool reset) {
