@@ -41,6 +41,7 @@
 // (PassArgs::balanced), which sends every pixel to the exact re-pass.
 #pragma once
 #include <cstdint>
+#include <type_traits>
 
 #include "pbr_device_math.h"
 #include "pbr_device_math_x2.h"
@@ -53,9 +54,6 @@ constexpr int kBalRec = 7;         // float4 per exchanged pixel record
 // Per-wave LDS: the exchange region (one record per lane, then the 128 results) and the count histogram.
 #ifndef PBR_BAL_EXPERIMENT
 #define PBR_BAL_EXPERIMENT 0  // development timing switches (0 = product)
-#endif
-#ifndef PBR_BAL_PIPELINE
-#define PBR_BAL_PIPELINE 0  // pass 2 reads the next pair's lights ahead (measured slower: 1.69 vs 1.01 ms)
 #endif
 #ifndef PBR_BAL_PROFILE
 #define PBR_BAL_PROFILE 0  // development build: per-phase shader-clock sums (pbr_debug_bal_profile)
@@ -162,6 +160,76 @@ __device__ __forceinline__ ItemPixel load_item(const float4* src) {
     return p;
 }
 
+// The exact (default-mode) record: the unscaled lean-loop invariants of make_invariants, less the three that
+// are one subtraction from another field (1 - F0, a^2 - 1, 1 - k: re-derived by load_item_x with the same
+// operation, so bit for bit the same values), and the pixel's sum so far (its directional lights), from which
+// the evaluating lane continues in the reference's order.
+struct ItemPixelX {
+    f3 pos, n, v, albedo, f0, omf0, start;
+    float omm, a_sqr, a2m1, k, omk, ggx_v, nv4;
+    uint32_t live0, live1;
+    int origin;
+};
+
+__device__ __forceinline__ ItemPixelX item_pixel_x(const PixelInvariants2& q, const f3x2& pos, const f3x2& start,
+                                                   int e, uint32_t live0, uint32_t live1, int origin) {
+    ItemPixelX r;
+    r.pos = lane(pos, e);
+    r.n = lane(q.n, e);
+    r.v = lane(q.v, e);
+    r.albedo = lane(q.albedo, e);
+    r.f0 = lane(q.f0, e);
+    r.start = lane(start, e);
+    r.omm = e ? q.one_minus_metal.y : q.one_minus_metal.x;
+    r.a_sqr = e ? q.a_sqr.y : q.a_sqr.x;
+    r.k = e ? q.k.y : q.k.x;
+    r.ggx_v = e ? q.ggx_v.y : q.ggx_v.x;
+    r.nv4 = e ? q.four_n_dot_v.y : q.four_n_dot_v.x;
+    r.live0 = live0;
+    r.live1 = live1;
+    r.origin = origin;
+    return r;
+}
+
+__device__ __forceinline__ void store_item(float4* dst, const ItemPixelX& p) {
+    dst[0] = make_float4(p.pos.x, p.pos.y, p.pos.z, p.n.x);
+    dst[1] = make_float4(p.n.y, p.n.z, p.v.x, p.v.y);
+    dst[2] = make_float4(p.v.z, p.albedo.x, p.albedo.y, p.albedo.z);
+    dst[3] = make_float4(p.f0.x, p.f0.y, p.f0.z, p.omm);
+    dst[4] = make_float4(p.a_sqr, p.k, p.ggx_v, p.nv4);
+    dst[5] = make_float4(p.start.x, p.start.y, p.start.z, __uint_as_float(p.live0));
+    dst[6] = make_float4(__uint_as_float(p.live1), __int_as_float(p.origin), 0.0f, 0.0f);
+}
+__device__ __forceinline__ ItemPixelX load_item_x(const float4* src) {
+    const float4 a = src[0], b = src[1], c = src[2], d = src[3], e = src[4], f = src[5], g = src[6];
+    ItemPixelX p;
+    p.pos = mk3(a.x, a.y, a.z);
+    p.n = mk3(a.w, b.x, b.y);
+    p.v = mk3(b.z, b.w, c.x);
+    p.albedo = mk3(c.y, c.z, c.w);
+    p.f0 = mk3(d.x, d.y, d.z);
+    p.omm = d.w;
+    p.a_sqr = e.x;
+    p.k = e.y;
+    p.ggx_v = e.z;
+    p.nv4 = e.w;
+    p.start = mk3(f.x, f.y, f.z);
+    p.live0 = __float_as_uint(f.w);
+    p.live1 = __float_as_uint(g.x);
+    p.origin = __float_as_int(g.y);
+    p.omf0 = mk3(1.0f - p.f0.x, 1.0f - p.f0.y, 1.0f - p.f0.z);  // make_invariants' operations
+    p.a2m1 = p.a_sqr - 1.0f;
+    p.omk = 1.0f - p.k;
+    return p;
+}
+template <bool EXACT>
+__device__ __forceinline__ auto load_item_any(const float4* src) {
+    if constexpr (EXACT)
+        return load_item_x(src);
+    else
+        return load_item(src);
+}
+
 // LDS traffic of one wave between its own lanes: the hardware executes a wave's LDS instructions in order;
 // the fences keep the compiler from moving them across this point.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -252,11 +320,36 @@ __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const 
     sum.z = vfma(vfma(kr, f.z, vfma(-f.z, splat(q.mab.z), splat(q.mab.z))), ls.z * w, sum.z);
 }
 
-// The whole balanced pass over point lights [b0, b1) (b1 - b0 <= kBalMaxLights) of an untiled faithful lean
-// wave. q / fi are the pair's scaled invariants (faithful_scale), `live_a` / `live_b` say which of the pair's
-// pixels take part (geometry). Adds each pixel's point-light sum into `sum` (any order is within the faithful
-// bound) and ORs the pixels that left the fast-path window into `redo`. Wave-uniform control
-// flow; no block barrier.
+// The same two items on the exact lean loop: point_or_spot_x2<false, true> (pbr_device_math_x2.h) for one pixel
+// and two lights, element for element the same operations (the pixel's invariants splat into both elements), so
+// each element's term carries the bits of the uniform loop's term for that (pixel, light).
+__device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3x2& lp, const f3x2& ls, m2& ok) {
+    PixelInvariants2 q;
+    q.n = splat3(p.n.x, p.n.y, p.n.z);
+    q.v = splat3(p.v.x, p.v.y, p.v.z);
+    q.albedo = splat3(p.albedo.x, p.albedo.y, p.albedo.z);
+    q.f0 = splat3(p.f0.x, p.f0.y, p.f0.z);
+    q.one_minus_f0 = splat3(p.omf0.x, p.omf0.y, p.omf0.z);
+    q.one_minus_metal = splat(p.omm);
+    q.a_sqr = splat(p.a_sqr);
+    q.a_sqr_minus_1 = splat(p.a2m1);
+    q.k = splat(p.k);
+    q.one_minus_k = splat(p.omk);
+    q.ggx_v = splat(p.ggx_v);
+    q.four_n_dot_v = splat(p.nv4);
+    q.f0_nonzero = m2{~0ull, ~0ull};  // not read by the lean BRDF
+    f3x2 l = f3x2{lp.x - p.pos.x, lp.y - p.pos.y, lp.z - p.pos.z};
+    const v2 dist = sqrt_nr(dot3(l, l));
+    ok &= ge(dist, 0x1p-20f);
+    const Recip2 rdist = recip_nr(dist);
+    l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
+    const f3x2 h = normalize_x2(add3(q.v, l), ok);
+    const v2 dsat = max_dsat(dist);
+    v2 att = recip_nr(dsat * dsat).r;
+    att *= in_range01(dist);
+    return brdf_x2<true>(q, f3x2{ls.x * att, ls.y * att, ls.z * att}, l, h, ok);
+}
+
 // The live-light masks of the pair's pixels (pass 1), light j at bit j % 32 of word j / 32.
 struct BalMasks {
     uint32_t a0, a1, c0, c1;  // pixel a: lights [0, 32), [32, 64); pixel b: the same
@@ -352,8 +445,15 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
     return BalMasks{a0, a1, c0, c1};
 }
 
-// `lds_lights`: the pass's point lights [b0, b1) staged by the block (stage_balanced_lights); `bm`: their live
-// masks from balanced_pass1.
+// The whole balanced pass over the point lights of an untiled lean wave (at most kBalMaxLights). `live_a` /
+// `live_b` say which of the pair's pixels take part (geometry); `lds_lights`: the pass's point lights staged by
+// the block (stage_balanced_lights); `bm`: their live masks from balanced_pass1. ORs the pixels that left the
+// fast-path window for a live item into `redo`. Wave-uniform control flow; no block barrier.
+// EXACT (the default mode's lean loop, bit-identical to the uniform loop): q is unscaled, `sum` holds the pair's
+// directional-light sums on entry; each pixel's sum continues from it through its live lights in increasing
+// light order (element 0 of an iteration is the smaller light; the skipped terms are the +-0 the reference adds),
+// and `sum` is replaced by the result. Faithful: q / fi scaled, the point-light sums are added into `sum`.
+template <bool EXACT>
 __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2& q, const Faithful2& fi,
                                                          const f3x2& pos, bool live_a, bool live_b, BalMasks bm,
                                                          BalancedWaveLds& w, const float* lds_lights, f3x2& sum,
@@ -382,13 +482,20 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     wave_lds_sync();
     const int rank_a = w.hist[bin_a] + pos_a, rank_b = w.hist[bin_b] + pos_b;
     // rank r < 64 -> lane r, first pixel; r >= 64 -> lane 127 - r, second pixel.
-    const ItemPixel ia = item_pixel(q, fi, pos, 0, a0, a1, 2 * lane_id);
-    const ItemPixel ib = item_pixel(q, fi, pos, 1, c0, c1, 2 * lane_id + 1);
+    using Item = std::conditional_t<EXACT, ItemPixelX, ItemPixel>;
+    Item ia, ib;
+    if constexpr (EXACT) {
+        ia = item_pixel_x(q, pos, sum, 0, a0, a1, 2 * lane_id);
+        ib = item_pixel_x(q, pos, sum, 1, c0, c1, 2 * lane_id + 1);
+    } else {
+        ia = item_pixel(q, fi, pos, 0, a0, a1, 2 * lane_id);
+        ib = item_pixel(q, fi, pos, 1, c0, c1, 2 * lane_id + 1);
+    }
     // Phase 0: the small-count pixels.
     if (rank_a < 64) store_item(&w.rec[kBalRec * rank_a], ia);
     if (rank_b < 64) store_item(&w.rec[kBalRec * rank_b], ib);
     wave_lds_sync();
-    ItemPixel cur = load_item(&w.rec[kBalRec * lane_id]);
+    Item cur = load_item_any<EXACT>(&w.rec[kBalRec * lane_id]);
     wave_lds_sync();
     // Phase 1: the large-count pixels stay in LDS; a lane reads its second pixel when it switches.
     if (rank_a >= 64) store_item(&w.rec[kBalRec * (127 - rank_a)], ia);
@@ -399,19 +506,23 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     // ---- pass 2
     // Window results are per-lane bools here: the loop body runs under a partial exec mask, where a lane
     // mask (m2, a ballot) has no bits for the inactive lanes -- ANDing it into a running mask would clear them.
+    // Faithful: two interleaved partial sums (acc); exact: one running sum per pixel (accx) in light order.
     f3x2 acc = splat3(0.0f, 0.0f, 0.0f);
+    f3 accx = mk3(0.0f, 0.0f, 0.0f);
+    if constexpr (EXACT) accx = cur.start;
     f3 acc_first = mk3(0.0f, 0.0f, 0.0f);
     bool ok = true, ok_first = true;
     int origin_first = cur.origin;
     bool second = false;
     uint64_t m = ((uint64_t)cur.live1 << 32) | cur.live0;
     auto next_pixel = [&]() {  // divergent: the lanes whose first pixel is done
-        acc_first = mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
+        acc_first = EXACT ? accx : mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
         ok_first = ok;
         origin_first = cur.origin;
-        cur = load_item(&w.rec[kBalRec * lane_id]);
+        cur = load_item_any<EXACT>(&w.rec[kBalRec * lane_id]);
         m = ((uint64_t)cur.live1 << 32) | cur.live0;
         acc = splat3(0.0f, 0.0f, 0.0f);
+        if constexpr (EXACT) accx = cur.start;
         ok = true;
         second = true;
     };
@@ -424,60 +535,6 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     if (!second) next_pixel();
     m = 0;
 #endif
-#if PBR_BAL_PIPELINE
-    // Software pipelined: the light records of a lane's next pair are read from LDS before the current pair's
-    // arithmetic (the waves run this loop nearly in step; a read waited on at once idles the SIMD).
-    const float* L = lds_lights;
-    constexpr int S = kBalLdsStride;
-    // The next pair of lights of the current pixel: j0 < j1; one light left -> j1 = j0 with the zero strength
-    // (s1 = kBalMaxLights): the second element then adds +0.
-    auto pop2 = [&](int& j0, int& j1, int& s1) {
-        j0 = __builtin_ctzll(m);
-        m &= m - 1;
-        const bool two = m != 0;
-        j1 = two ? __builtin_ctzll(m) : j0;
-        m &= two ? m - 1 : m;
-        s1 = two ? j1 : kBalMaxLights;
-    };
-    auto fetch = [&](int j0, int j1, int s1, f3x2& lp, f3x2& ls) {
-        lp = f3x2{v2{L[j0], L[j1]}, v2{L[S + j0], L[S + j1]}, v2{L[2 * S + j0], L[2 * S + j1]}};
-        ls = f3x2{v2{L[3 * S + j0], L[3 * S + s1]}, v2{L[4 * S + j0], L[4 * S + s1]}, v2{L[5 * S + j0], L[5 * S + s1]}};
-    };
-    bool has = m != 0;  // the lane has a current pair
-    f3x2 lp{}, ls{};
-    {
-        int j0 = 0, j1 = 0, s1 = kBalMaxLights;
-        if (has) pop2(j0, j1, s1);
-        fetch(j0, j1, s1, lp, ls);
-    }
-    while (__builtin_amdgcn_ballot_w64(has) != 0) {
-#if PBR_BAL_PROFILE
-        ++iters;
-#endif
-        if (has) {
-            const bool more = m != 0;
-            int k0 = 0, k1 = 0, t1 = kBalMaxLights;  // without a next pair: harmless reads of light 0
-            if (more) pop2(k0, k1, t1);
-            f3x2 np, ns;
-            fetch(k0, k1, t1, np, ns);
-            m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests; only this lane's bits are read
-            faithful_point_items2(cur, lp, ls, oki, acc);
-            ok = ok && on(oki.x) && on(oki.y);
-            lp = np;
-            ls = ns;
-            has = more;
-            if (!has && !second) {
-                next_pixel();
-                has = m != 0;
-                if (has) {
-                    int j0, j1, s1;
-                    pop2(j0, j1, s1);
-                    fetch(j0, j1, s1, lp, ls);
-                }
-            }
-        }
-    }
-#else
     while (true) {
         const bool active = m != 0;
         if (__builtin_amdgcn_ballot_w64(active) == 0) break;
@@ -494,14 +551,18 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
             m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests; only this lane's bits are read
             f3x2 lp, ls;
             read_pair_lights(lds_lights, j0, j1, s1, lp, ls);
-            faithful_point_items2(cur, lp, ls, oki, acc);
+            if constexpr (EXACT) {
+                const f3x2 c = exact_point_items2(cur, lp, ls, oki);
+                accx = mk3((accx.x + c.x.x) + c.x.y, (accx.y + c.y.x) + c.y.y, (accx.z + c.z.x) + c.z.y);
+            } else {
+                faithful_point_items2(cur, lp, ls, oki, acc);
+            }
             ok = ok && on(oki.x) && on(oki.y);
             if (m == 0 && !second) next_pixel();
         }
     }
-#endif
     BAL_PROF_T(t3);
-    const f3 acc_second = mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
+    const f3 acc_second = EXACT ? accx : mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
     const bool ok_second = ok;
     // Every lane is on its second pixel now: a lane switches when its first pixel has no live light left,
     // and the loop runs until no lane has one.
@@ -513,7 +574,10 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     wave_lds_sync();
     const float4 ra = w.rec[2 * lane_id], rb = w.rec[2 * lane_id + 1];
     wave_lds_sync();
-    sum = f3x2{sum.x + v2{ra.x, rb.x}, sum.y + v2{ra.y, rb.y}, sum.z + v2{ra.z, rb.z}};
+    if constexpr (EXACT)
+        sum = f3x2{v2{ra.x, rb.x}, v2{ra.y, rb.y}, v2{ra.z, rb.z}};
+    else
+        sum = f3x2{sum.x + v2{ra.x, rb.x}, sum.y + v2{ra.y, rb.y}, sum.z + v2{ra.z, rb.z}};
     redo |= mask2(live_a && ra.w == 0.0f, live_b && rb.w == 0.0f);
 #if PBR_BAL_PROFILE
     BAL_PROF_T(t4);

@@ -50,8 +50,8 @@ struct pbr_context {
     int64_t last_tiles = 0;
     int64_t last_slots = 0;  // statistics records of the last pass (shade_stat_slots_per_tile per tile)
     bool last_culled = false;
-    // Wave-balanced point-light lists (pbr_balanced.h) for untiled faithful passes with at least this many
-    // point lights and no spot lights; PBR_BALANCED_MIN overrides (0 disables).
+    // Wave-balanced point-light lists (pbr_balanced.h) for untiled passes with at least this many point lights
+    // and no spot lights; PBR_BALANCED_MIN overrides (0 disables).
     int balanced_min = 16;
     bool points_flag_ok = false;  // pbr_set_pass: every point light inside the fast-path window
     int pixels_per_thread = 2;  // kernel layout: packed pixel pairs (measured faster); PBR_PIXELS_PER_THREAD=1 overrides
@@ -365,9 +365,13 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
                     (ctx->ambient_mode != PBR_AMBIENT_IBL_DIFFUSE || ctx->env.nonneg);
     if (a.ps.faithful && ctx->faithful_count_terms) a.ps.faithful = 2;
     a.pixels_per_thread = ctx->pixels_per_thread;
-    a.ps.balanced = a.ps.faithful == 1 && !cull && a.pixels_per_thread == 2 && ctx->balanced_min > 0 &&
-                    ctx->points_flag_ok &&
-                    a.ps.n_spot == 0 && a.ps.n_point >= ctx->balanced_min && a.ps.n_point <= pbr::kBalMaxLights;
+    // Wave-balanced point-light lists: untiled pair-kernel passes with only point lights after the directional
+    // ones, every one inside the fast-path window; faithful (1) or exact (2) -- the exact variant keeps the
+    // reference's order per pixel (bit-identical), the faithful one re-associates (a culled faithful pass with
+    // counted terms, faithful == 2, keeps the uniform loop).
+    const bool bal_ok = !cull && a.pixels_per_thread == 2 && ctx->balanced_min > 0 && ctx->points_flag_ok &&
+                        a.ps.n_spot == 0 && a.ps.n_point >= ctx->balanced_min && a.ps.n_point <= pbr::kBalMaxLights;
+    a.ps.balanced = !bal_ok ? 0 : a.ps.faithful == 1 ? 1 : a.ps.faithful == 0 && !a.exact_only ? 2 : 0;
 
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;

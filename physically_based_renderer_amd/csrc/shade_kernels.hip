@@ -244,7 +244,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     // BALANCED passes have no spot lights (host: PassArgs::balanced): nothing reads q or pos after the
     // balanced loop, so the caller can drop them across it.
     if (BALANCED)
-        lighting_balanced_points(q, fi, pos, geo_a, geo_b, bm, *bal, bal_lights, direct, redo, bal_prof);
+        lighting_balanced_points<!FAITHFUL>(q, fi, pos, geo_a, geo_b, bm, *bal, bal_lights, direct, redo, bal_prof);
     else
         run_kind(std::false_type{}, pt_begin, sp_begin);
     if (!BALANCED && end > sp_begin) run_kind(std::true_type{}, sp_begin, end);
@@ -508,9 +508,10 @@ __device__ __forceinline__ int lane_id_fresh() {
 
 }  // namespace
 
-// BAL (untiled only): the variant whose faithful lean waves take the wave-balanced point-light lists
-// (pbr_balanced.h); a separate instantiation so that the other variants' register allocation is untouched.
-template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, bool BAL = false>
+// BAL (untiled only; PassArgs::balanced): the variant whose lean waves take the wave-balanced point-light lists
+// (pbr_balanced.h) -- 1: faithful passes, 2: exact passes; separate instantiations so that the other variants'
+// register allocation is untouched.
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, int BAL = 0>
 __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GBufferArgs gb, PassArgs ps,
                                                             const float4* __restrict__ lights,
                                                             const float4* __restrict__ env, FrameArgs fr,
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     if ((threadIdx.x & 63) < 16) bal_prof[threadIdx.x & 63] = 0;
 #endif
     load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
-    if constexpr (BAL) stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light);
+    if constexpr (BAL != 0) stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light);
     __syncthreads();
 
     const int tid = threadIdx.x;
@@ -599,7 +600,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         // Untiled faithful waves read rescaled invariants (exact both ways, faithful_scale).
         if (faithful_wave && lean_wave) {
             if (!CULL) faithful_scale(q2);
-            if constexpr (BAL && !CULL) {
+            if constexpr (BAL == 1 && !CULL) {
 #if PBR_BAL_PROFILE
                 BAL_PROF_ADD(7, (long long)__builtin_amdgcn_s_memtime() - t_entry);
                 unsigned long long* prof = s.prof[wave_id];
@@ -646,9 +647,27 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             if (!CULL) faithful_scale(q2);
             d2 = lighting_fast<CULL, false, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
             if (!CULL) faithful_unscale(q2);
-        } else if (lean_wave)
-            d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
-        else
+        } else if (lean_wave) {
+            if constexpr (BAL == 2 && !CULL) {
+#if PBR_BAL_PROFILE
+                unsigned long long* prof = s.prof[wave_id];
+#else
+                unsigned long long* prof = nullptr;
+#endif
+                // As in the faithful branch: pass 1 on the raw pair, the invariants rebuilt around the loop.
+                const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, s.bal[wave_id], s.bal_light, prof);
+                launder(p);
+                q2 = pair_invariants(p, ps, fast2);
+                d2 = lighting_fast<false, true, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
+                                                             kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
+                                                             prof);
+                launder(p);
+                q2 = pair_invariants(p, ps, fast2);
+                pos2 = p.pos;
+            } else {
+                d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+            }
+        } else
             d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
     }
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
@@ -846,8 +865,11 @@ template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
     if (a.pixels_per_thread == 2) {
         dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
-        if (!CULL && a.ps.balanced)
-            hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, true>), grid, dim3(kBlock), 0,
+        if (!CULL && a.ps.balanced == 1)
+            hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 1>), grid, dim3(kBlock), 0,
+                               stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
+        else if (!CULL && a.ps.balanced == 2)
+            hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 2>), grid, dim3(kBlock), 0,
                                stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
         else
             hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,

@@ -1,11 +1,14 @@
 """Wave-balanced point-light lists (pbr_balanced.h): back-face rejection + cross-lane rebalancing.
 
-The balanced kernel evaluates each live (pixel, light) item with the same operations as the packed faithful
-loop and skips only items whose reference term is +-0; it sums each pixel's live terms in two interleaved
-partial sums, so its frames differ from the unbalanced faithful kernel's by the association of the sum
-only: both must be within the north-star 1e-5 of the oracle, and within a few ulps of each other. The
-contexts here choose the path through PBR_BALANCED_MIN, which pbr_context_create reads (0 = never
-balanced, 1 = every untiled faithful pass with point lights only).
+The balanced kernel evaluates each live (pixel, light) item with the same operations as the packed uniform
+loop and skips only items whose reference term is +-0.
+* Faithful passes: it sums each pixel's live terms in two interleaved partial sums, so its frames differ from
+  the unbalanced faithful kernel's by the association of the sum only: both must be within the north-star
+  1e-5 of the oracle, and within a few ulps of each other.
+* Exact (default) passes: each pixel's sum continues from its directional lights through its live point
+  lights in light order, so the frames are bit-identical to the unbalanced kernel's and to the oracle's.
+The contexts here choose the path through PBR_BALANCED_MIN, which pbr_context_create reads (0 = never
+balanced, 1 = every untiled pass with point lights only).
 """
 import numpy as np
 import pytest
@@ -49,6 +52,24 @@ def ctx_pair(gpu):
 
 def faithful(pc):
     return PassConstants(**{**pc.__dict__, "flags": pc.flags | N.PBR_FLAG_FAITHFUL})
+
+
+def exact(pc):
+    return PassConstants(**{**pc.__dict__, "flags": pc.flags & ~N.PBR_FLAG_FAITHFUL})
+
+
+MODES = ["faithful", "exact"]
+
+
+def check_mode(mode, got, want, ref):
+    """Faithful: the association bound against the unbalanced frame and 1e-5 against the oracle; exact: the
+    same bits as both (NaN payloads aside)."""
+    if mode == "exact":
+        assert O.bit_equal(got, want).all()
+        assert O.bit_equal(got, ref).all()
+    else:
+        assert close(got, want)
+        assert O.rel_err(got, ref).max() <= REL_TOL
 
 
 def run(ctx, gb, pc, env=None):
@@ -99,7 +120,8 @@ def _scene(rng, w, h, n_lights):
     return planes, lights
 
 
-def test_balanced_back_face_edges(ctx_pair, gpu):
+@pytest.mark.parametrize("mode", MODES)
+def test_balanced_back_face_edges(mode, ctx_pair, gpu):
     """Items at the edges of the back-face test:
     * L == -V exactly (eye, pixel and light collinear, pixel facing the eye): the reference's
       H = normalize(V + L) is NaN, but max(dot(N, H), 0) and saturate(dot(H, V)) map it to 0 and with
@@ -134,33 +156,73 @@ def test_balanced_back_face_edges(ctx_pair, gpu):
     planes[3:6, 3, 0] = (0.0, 0.0, -1.0)
     lights[9, 8:11] = (1.0, 1.0, 1.001)
     lights[10, 8:11] = (1.0, 1.0, 151.0)
-    pc = PassConstants(eye_pos_w=tuple(eye), num_point_lights=nl, lights_array=lights, flags=N.PBR_FLAG_FAITHFUL)
+    flags = N.PBR_FLAG_FAITHFUL if mode == "faithful" else 0
+    pc = PassConstants(eye_pos_w=tuple(eye), num_point_lights=nl, lights_array=lights, flags=flags)
     gb = GBuffer.from_host(planes, gpu)
     bal, plain = ctx_pair
     got, redo_b = run(bal, gb, pc)
     want, redo_p = run(plain, gb, pc)
     ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
-    print(f"edges: redo {redo_b} vs {redo_p}; NaN pixels {int(np.isnan(ref[..., 0]).sum())}")
+    print(f"edges ({mode}): redo {redo_b} vs {redo_p}; NaN pixels {int(np.isnan(ref[..., 0]).sum())}")
     assert np.isfinite(ref[0, :16]).all()  # the L == -V pixels: the NaN H is absorbed by maxNum
     assert np.array_equal(np.isnan(got), np.isnan(ref))
-    assert close(got, want)
     assert redo_b <= redo_p
-    assert O.rel_err(got, ref).max() <= REL_TOL
+    check_mode(mode, got, want, ref)
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("n_lights", [1, 31, 32, 33, 63, 64])
-def test_balanced_light_counts(n_lights, ctx_pair, gpu):
+def test_balanced_light_counts(n_lights, mode, ctx_pair, gpu):
     """Mask-word boundaries (32 lights per word) and the one-light pass."""
     rng = np.random.default_rng(100 + n_lights)
     planes, lights = _scene(rng, 256, 8, n_lights)
-    pc = PassConstants(num_point_lights=n_lights, lights_array=lights, flags=N.PBR_FLAG_FAITHFUL)
+    flags = N.PBR_FLAG_FAITHFUL if mode == "faithful" else 0
+    pc = PassConstants(num_point_lights=n_lights, lights_array=lights, flags=flags)
     gb = GBuffer.from_host(planes, gpu)
     bal, plain = ctx_pair
     got, _ = run(bal, gb, pc)
     want, _ = run(plain, gb, pc)
     ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
-    assert close(got, want)
-    assert O.rel_err(got, ref).max() <= REL_TOL
+    check_mode(mode, got, want, ref)
+
+
+@pytest.mark.parametrize("cid,size", [(2, (1920, 256)), (3, (1024, 256)), (3, (1000, 77))])
+def test_balanced_exact_scene_configs(cid, size, ctx_pair, gpu, env_map):
+    """Exact (default) passes of the scene configs: bit-identical to the uniform loop and to the oracle."""
+    cfg = S.CONFIGS[cid].with_size(*size)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = exact(S.scene_pass(cfg))
+    env = env_map if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc, env)
+    want, redo_p = run(plain, gb, pc, env)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), env, n_threads=16)
+    print(f"{cfg.name} {cfg.width}x{cfg.height} exact: redo {redo_b} vs {redo_p}")
+    assert redo_b <= redo_p
+    check_mode("exact", got, want, ref)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_balanced_after_directional_lights(mode, ctx_pair, gpu):
+    """Directional lights ahead of the point lights: the exact pass continues each pixel's sum from its
+    directional terms (the record's start value), in the reference's order."""
+    rng = np.random.default_rng(11)
+    nd, npt = 3, 40
+    planes, lights = _scene(rng, 384, 8, nd + npt)
+    d = rng.normal(size=(nd, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    lights[:nd, 4:7] = d
+    lights[:nd, 8:11] = 0.0
+    flags = N.PBR_FLAG_FAITHFUL if mode == "faithful" else 0
+    pc = PassConstants(num_dir_lights=nd, num_point_lights=npt, lights_array=lights, flags=flags)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc)
+    want, redo_p = run(plain, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    assert redo_b <= redo_p
+    check_mode(mode, got, want, ref)
 
 
 def test_balanced_light_outside_window_sends_all_to_exact(ctx_pair, gpu):
