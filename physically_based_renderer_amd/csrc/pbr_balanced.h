@@ -96,10 +96,20 @@ __device__ __forceinline__ void stage_balanced_lights(const float4* __restrict__
     }
 }
 
+constexpr int kBalRecX = 6;        // float4 per exchanged pixel record, exact passes
+
 struct BalancedWaveLds {
     float4 rec[64 * kBalRec];  // 7 KiB
-    float4 bound[16];          // pass 1: the lights' distance bounds B_j (64 floats)
-    int hist[64];
+    union {
+        struct {
+            float4 bound[16];  // pass 1: the lights' distance bounds B_j (64 floats)
+            int hist[64];      // ranking
+        };
+        int flag[128];         // pass 2 results: the pixel stayed inside the fast-path window, by origin
+    };
+    // By origin: exact passes, each pixel's sum before its point lights (written by the owner); then the
+    // pixel's result (written by the evaluating lane once the pixel is done, after it has read the start).
+    float start[3][128];
 };
 
 // The per-pixel loop invariants of the faithful scaled lean loop (the scalar view of PixelInvariants2 after
@@ -162,24 +172,24 @@ __device__ __forceinline__ ItemPixel load_item(const float4* src) {
 
 // The exact (default-mode) record: the unscaled lean-loop invariants of make_invariants, less the three that
 // are one subtraction from another field (1 - F0, a^2 - 1, 1 - k: re-derived by load_item_x with the same
-// operation, so bit for bit the same values), and the pixel's sum so far (its directional lights), from which
-// the evaluating lane continues in the reference's order.
+// operation, so bit for bit the same values). The pixel's sum so far (its directional lights), from which the
+// evaluating lane continues in the reference's order, travels separately (BalancedWaveLds::start): written by
+// the owner before the exchange, it is not held in registers through it.
 struct ItemPixelX {
-    f3 pos, n, v, albedo, f0, omf0, start;
+    f3 pos, n, v, albedo, f0, omf0;
     float omm, a_sqr, a2m1, k, omk, ggx_v, nv4;
     uint32_t live0, live1;
     int origin;
 };
 
-__device__ __forceinline__ ItemPixelX item_pixel_x(const PixelInvariants2& q, const f3x2& pos, const f3x2& start,
-                                                   int e, uint32_t live0, uint32_t live1, int origin) {
+__device__ __forceinline__ ItemPixelX item_pixel_x(const PixelInvariants2& q, const f3x2& pos, int e, uint32_t live0,
+                                                   uint32_t live1, int origin) {
     ItemPixelX r;
     r.pos = lane(pos, e);
     r.n = lane(q.n, e);
     r.v = lane(q.v, e);
     r.albedo = lane(q.albedo, e);
     r.f0 = lane(q.f0, e);
-    r.start = lane(start, e);
     r.omm = e ? q.one_minus_metal.y : q.one_minus_metal.x;
     r.a_sqr = e ? q.a_sqr.y : q.a_sqr.x;
     r.k = e ? q.k.y : q.k.x;
@@ -197,11 +207,10 @@ __device__ __forceinline__ void store_item(float4* dst, const ItemPixelX& p) {
     dst[2] = make_float4(p.v.z, p.albedo.x, p.albedo.y, p.albedo.z);
     dst[3] = make_float4(p.f0.x, p.f0.y, p.f0.z, p.omm);
     dst[4] = make_float4(p.a_sqr, p.k, p.ggx_v, p.nv4);
-    dst[5] = make_float4(p.start.x, p.start.y, p.start.z, __uint_as_float(p.live0));
-    dst[6] = make_float4(__uint_as_float(p.live1), __int_as_float(p.origin), 0.0f, 0.0f);
+    dst[5] = make_float4(__uint_as_float(p.live0), __uint_as_float(p.live1), __int_as_float(p.origin), 0.0f);
 }
 __device__ __forceinline__ ItemPixelX load_item_x(const float4* src) {
-    const float4 a = src[0], b = src[1], c = src[2], d = src[3], e = src[4], f = src[5], g = src[6];
+    const float4 a = src[0], b = src[1], c = src[2], d = src[3], e = src[4], f = src[5];
     ItemPixelX p;
     p.pos = mk3(a.x, a.y, a.z);
     p.n = mk3(a.w, b.x, b.y);
@@ -213,10 +222,9 @@ __device__ __forceinline__ ItemPixelX load_item_x(const float4* src) {
     p.k = e.y;
     p.ggx_v = e.z;
     p.nv4 = e.w;
-    p.start = mk3(f.x, f.y, f.z);
-    p.live0 = __float_as_uint(f.w);
-    p.live1 = __float_as_uint(g.x);
-    p.origin = __float_as_int(g.y);
+    p.live0 = __float_as_uint(f.x);
+    p.live1 = __float_as_uint(f.y);
+    p.origin = __float_as_int(f.z);
     p.omf0 = mk3(1.0f - p.f0.x, 1.0f - p.f0.y, 1.0f - p.f0.z);  // make_invariants' operations
     p.a2m1 = p.a_sqr - 1.0f;
     p.omk = 1.0f - p.k;
@@ -460,7 +468,9 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
                                                          m2& redo, unsigned long long* bal_prof = nullptr) {
     const int lane_id = (int)(threadIdx.x & 63);
     const uint32_t a0 = bm.a0, a1 = bm.a1, c0 = bm.c0, c1 = bm.c1;
+    constexpr int R = EXACT ? kBalRecX : kBalRec;  // record stride (float4)
     BAL_PROF_T(t1);
+
     // ---- rank the wave's 128 pixels by live count (counting sort; ties in LDS-atomic order, which only
     // decides which lane evaluates a pixel, never how)
     const int cnt_a = __popc(a0) + __popc(a1), cnt_b = __popc(c0) + __popc(c1);
@@ -485,21 +495,21 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     using Item = std::conditional_t<EXACT, ItemPixelX, ItemPixel>;
     Item ia, ib;
     if constexpr (EXACT) {
-        ia = item_pixel_x(q, pos, sum, 0, a0, a1, 2 * lane_id);
-        ib = item_pixel_x(q, pos, sum, 1, c0, c1, 2 * lane_id + 1);
+        ia = item_pixel_x(q, pos, 0, a0, a1, 2 * lane_id);
+        ib = item_pixel_x(q, pos, 1, c0, c1, 2 * lane_id + 1);
     } else {
         ia = item_pixel(q, fi, pos, 0, a0, a1, 2 * lane_id);
         ib = item_pixel(q, fi, pos, 1, c0, c1, 2 * lane_id + 1);
     }
     // Phase 0: the small-count pixels.
-    if (rank_a < 64) store_item(&w.rec[kBalRec * rank_a], ia);
-    if (rank_b < 64) store_item(&w.rec[kBalRec * rank_b], ib);
+    if (rank_a < 64) store_item(&w.rec[R * rank_a], ia);
+    if (rank_b < 64) store_item(&w.rec[R * rank_b], ib);
     wave_lds_sync();
-    Item cur = load_item_any<EXACT>(&w.rec[kBalRec * lane_id]);
+    Item cur = load_item_any<EXACT>(&w.rec[R * lane_id]);
     wave_lds_sync();
     // Phase 1: the large-count pixels stay in LDS; a lane reads its second pixel when it switches.
-    if (rank_a >= 64) store_item(&w.rec[kBalRec * (127 - rank_a)], ia);
-    if (rank_b >= 64) store_item(&w.rec[kBalRec * (127 - rank_b)], ib);
+    if (rank_a >= 64) store_item(&w.rec[R * (127 - rank_a)], ia);
+    if (rank_b >= 64) store_item(&w.rec[R * (127 - rank_b)], ib);
     wave_lds_sync();
 
     BAL_PROF_T(t2);
@@ -509,20 +519,24 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     // Faithful: two interleaved partial sums (acc); exact: one running sum per pixel (accx) in light order.
     f3x2 acc = splat3(0.0f, 0.0f, 0.0f);
     f3 accx = mk3(0.0f, 0.0f, 0.0f);
-    if constexpr (EXACT) accx = cur.start;
-    f3 acc_first = mk3(0.0f, 0.0f, 0.0f);
-    bool ok = true, ok_first = true;
-    int origin_first = cur.origin;
+    bool ok = true;
     bool second = false;
     uint64_t m = ((uint64_t)cur.live1 << 32) | cur.live0;
+    // A finished pixel's result goes to LDS at once (its start slot, read already, and its flag), so that
+    // nothing of the first pixel stays in registers through the second one's iterations.
+    auto put_result = [&]() {
+        const f3 r = EXACT ? accx : mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
+        w.start[0][cur.origin] = r.x;
+        w.start[1][cur.origin] = r.y;
+        w.start[2][cur.origin] = r.z;
+        w.flag[cur.origin] = ok ? 1 : 0;
+    };
     auto next_pixel = [&]() {  // divergent: the lanes whose first pixel is done
-        acc_first = EXACT ? accx : mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
-        ok_first = ok;
-        origin_first = cur.origin;
-        cur = load_item_any<EXACT>(&w.rec[kBalRec * lane_id]);
+        put_result();
+        cur = load_item_any<EXACT>(&w.rec[R * lane_id]);
         m = ((uint64_t)cur.live1 << 32) | cur.live0;
         acc = splat3(0.0f, 0.0f, 0.0f);
-        if constexpr (EXACT) accx = cur.start;
+        accx = mk3(0.0f, 0.0f, 0.0f);
         ok = true;
         second = true;
     };
@@ -562,23 +576,21 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
         }
     }
     BAL_PROF_T(t3);
-    const f3 acc_second = EXACT ? accx : mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
-    const bool ok_second = ok;
     // Every lane is on its second pixel now: a lane switches when its first pixel has no live light left,
     // and the loop runs until no lane has one.
-    const int origin_second = cur.origin;
+    put_result();
+    // ---- hand the results back: the owner reads its two pixels' (by origin 2 lane + element)
     wave_lds_sync();
-    // ---- hand the sums back: results at rec[origin] (128 float4), owner reads its two
-    w.rec[origin_first] = make_float4(acc_first.x, acc_first.y, acc_first.z, ok_first ? 1.0f : 0.0f);
-    w.rec[origin_second] = make_float4(acc_second.x, acc_second.y, acc_second.z, ok_second ? 1.0f : 0.0f);
-    wave_lds_sync();
-    const float4 ra = w.rec[2 * lane_id], rb = w.rec[2 * lane_id + 1];
+    const float2 rx = reinterpret_cast<const float2*>(w.start[0])[lane_id];
+    const float2 ry = reinterpret_cast<const float2*>(w.start[1])[lane_id];
+    const float2 rz = reinterpret_cast<const float2*>(w.start[2])[lane_id];
+    const int2 fl = reinterpret_cast<const int2*>(w.flag)[lane_id];
     wave_lds_sync();
     if constexpr (EXACT)
-        sum = f3x2{v2{ra.x, rb.x}, v2{ra.y, rb.y}, v2{ra.z, rb.z}};
+        sum = f3x2{v2{rx.x, rx.y}, v2{ry.x, ry.y}, v2{rz.x, rz.y}};
     else
-        sum = f3x2{sum.x + v2{ra.x, rb.x}, sum.y + v2{ra.y, rb.y}, sum.z + v2{ra.z, rb.z}};
-    redo |= mask2(live_a && ra.w == 0.0f, live_b && rb.w == 0.0f);
+        sum = f3x2{sum.x + v2{rx.x, rx.y}, sum.y + v2{ry.x, ry.y}, sum.z + v2{rz.x, rz.y}};
+    redo |= mask2(live_a && fl.x == 0, live_b && fl.y == 0);
 #if PBR_BAL_PROFILE
     BAL_PROF_T(t4);
     BAL_PROF_ADD(1, t2 - t1);

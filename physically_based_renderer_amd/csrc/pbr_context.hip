@@ -365,13 +365,15 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
                     (ctx->ambient_mode != PBR_AMBIENT_IBL_DIFFUSE || ctx->env.nonneg);
     if (a.ps.faithful && ctx->faithful_count_terms) a.ps.faithful = 2;
     a.pixels_per_thread = ctx->pixels_per_thread;
-    // Wave-balanced point-light lists: untiled pair-kernel passes with only point lights after the directional
-    // ones, every one inside the fast-path window; faithful (1) or exact (2) -- the exact variant keeps the
-    // reference's order per pixel (bit-identical), the faithful one re-associates (a culled faithful pass with
-    // counted terms, faithful == 2, keeps the uniform loop).
+    // Wave-balanced point-light lists: untiled pair-kernel passes with no spot lights, every point light inside
+    // the fast-path window; faithful (1) or exact (2, and no directional lights either) -- the exact variant
+    // keeps the reference's order per pixel (bit-identical), the faithful one re-associates.
     const bool bal_ok = !cull && a.pixels_per_thread == 2 && ctx->balanced_min > 0 && ctx->points_flag_ok &&
                         a.ps.n_spot == 0 && a.ps.n_point >= ctx->balanced_min && a.ps.n_point <= pbr::kBalMaxLights;
-    a.ps.balanced = !bal_ok ? 0 : a.ps.faithful == 1 ? 1 : a.ps.faithful == 0 && !a.exact_only ? 2 : 0;
+    a.ps.balanced = !bal_ok                                                ? 0
+                    : a.ps.faithful == 1                                   ? 1
+                    : a.ps.faithful == 0 && !a.exact_only && a.ps.n_dir == 0 ? 2
+                                                                           : 0;
 
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;

@@ -29,7 +29,7 @@ struct PassArgs {
     int sky_w, sky_h;
     int eye_ok;  // the eye position is inside the fast-path window (0 or |x| in [2^-20, 2^20]), host-checked
     int balanced;  // untiled pass whose point lights take the wave-balanced lists (pbr_balanced.h): 0 no,
-                   // 1 faithful pass, 2 exact pass (no spot lights)
+                   // 1 faithful pass (no spot lights), 2 exact pass (no spot or directional lights)
     int faithful;  // PBR_FLAG_FAITHFUL: 0 off; 1 on (host preconditions hold); 2 on, culled pass with > 64
                    // lights: the kernel counts each wave's summed terms against the bound's 64
 };

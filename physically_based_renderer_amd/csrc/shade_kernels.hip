@@ -195,7 +195,10 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     Faithful2 fi{};
     if (FAITHFUL) fi = make_faithful<!CULL>(q);
-    for (int j = 0; j < ps.n_dir; ++j) {  // directional: never culled
+    // Exact balanced passes have no directional lights (host: PassArgs::balanced == 2): their loop is compiled
+    // out there, it was the register peak of that path.
+    const int n_dir = BALANCED && !FAITHFUL ? 0 : ps.n_dir;
+    for (int j = 0; j < n_dir; ++j) {  // directional: never culled
         const LightRec r = light_rec(lights, j);
         m2 ok = fast_ok & light_flag(r);
         if (FAITHFUL) {
@@ -654,14 +657,24 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 #else
                 unsigned long long* prof = nullptr;
 #endif
-                // As in the faithful branch: pass 1 on the raw pair, the invariants rebuilt around the loop.
+                // Pass 1 on the raw pair, then the invariants for the loop. The exact loop's temporaries leave no
+                // room to carry the raw pair across it (it spilled: ~250 B/px of scratch traffic), so the pair is
+                // read from the G-buffer again afterwards (44 B/px; the memory clobber keeps the compiler from
+                // reusing the first load's registers).
                 const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, s.bal[wave_id], s.bal_light, prof);
                 launder(p);
                 q2 = pair_invariants(p, ps, fast2);
                 d2 = lighting_fast<false, true, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
                                                              kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
                                                              prof);
-                launder(p);
+                // The element offsets are re-derived from the hardware ids (lane_id_fresh): otherwise the compiler
+                // keeps the first load's 64-bit offsets or per-plane addresses live across the loop (spilled).
+                const int rl = lane_id_fresh();
+                const int rx = blockIdx.x * kTileW + 2 * (rl & 31), ry = blockIdx.y * kTileH + 2 * wave_id + (rl >> 5);
+                const int64_t rrow = (int64_t)ry * gb.row_stride + rx;
+                p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? rrow : 0, vb ? rrow + 1 : 0, vb && gb.pairs_aligned);
+                ao_a = p.ao.x;
+                ao_b = p.ao.y;
                 q2 = pair_invariants(p, ps, fast2);
                 pos2 = p.pos;
             } else {

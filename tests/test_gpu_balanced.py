@@ -205,8 +205,9 @@ def test_balanced_exact_scene_configs(cid, size, ctx_pair, gpu, env_map):
 
 @pytest.mark.parametrize("mode", MODES)
 def test_balanced_after_directional_lights(mode, ctx_pair, gpu):
-    """Directional lights ahead of the point lights: the exact pass continues each pixel's sum from its
-    directional terms (the record's start value), in the reference's order."""
+    """Directional lights ahead of the point lights: faithful passes add the balanced point-light sums to the
+    directional ones; exact passes keep the uniform loop (the host gate: the balanced exact variant has no
+    directional loop), so both modes must still match."""
     rng = np.random.default_rng(11)
     nd, npt = 3, 40
     planes, lights = _scene(rng, 384, 8, nd + npt)
