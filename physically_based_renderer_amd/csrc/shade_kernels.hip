@@ -657,22 +657,27 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 #else
                 unsigned long long* prof = nullptr;
 #endif
-                // Pass 1 on the raw pair, then the invariants for the loop. The exact loop's temporaries leave no
-                // room to carry the raw pair across it (it spilled: ~250 B/px of scratch traffic), so the pair is
-                // read from the G-buffer again afterwards (44 B/px; the memory clobber keeps the compiler from
-                // reusing the first load's registers).
+                // Nothing of the raw pair is carried through the loop: it is read from the G-buffer again
+                // afterwards (44 B/px). Carrying it spilled (~250 B/px of scratch traffic): the exact loop's
+                // temporaries leave no room for it. The offsets are re-derived from the hardware ids
+                // (lane_id_fresh) and the memory clobber keeps the compiler from reusing the first load.
+                // (Reading it once more after pass 1 too, so that only position and normal live through
+                // pass 1, removed the remaining scratch of this path but measured the same.)
+                auto reload = [&]() {
+                    asm volatile("" ::: "memory");
+                    const int rl = lane_id_fresh();
+                    const int rx = blockIdx.x * kTileW + 2 * (rl & 31);
+                    const int ry = blockIdx.y * kTileH + 2 * wave_id + (rl >> 5);
+                    const int64_t rrow = (int64_t)ry * gb.row_stride + rx;
+                    p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? rrow : 0, vb ? rrow + 1 : 0,
+                                                      vb && gb.pairs_aligned);
+                };
                 const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, s.bal[wave_id], s.bal_light, prof);
-                launder(p);
                 q2 = pair_invariants(p, ps, fast2);
                 d2 = lighting_fast<false, true, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
                                                              kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
                                                              prof);
-                // The element offsets are re-derived from the hardware ids (lane_id_fresh): otherwise the compiler
-                // keeps the first load's 64-bit offsets or per-plane addresses live across the loop (spilled).
-                const int rl = lane_id_fresh();
-                const int rx = blockIdx.x * kTileW + 2 * (rl & 31), ry = blockIdx.y * kTileH + 2 * wave_id + (rl >> 5);
-                const int64_t rrow = (int64_t)ry * gb.row_stride + rx;
-                p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? rrow : 0, vb ? rrow + 1 : 0, vb && gb.pairs_aligned);
+                reload();
                 ao_a = p.ao.x;
                 ao_b = p.ao.y;
                 q2 = pair_invariants(p, ps, fast2);
