@@ -9,14 +9,27 @@
 //   build/pbr_render --config 2 --dump frame.bin      # one frame -> file (tests compare it with the oracle)
 //   build/pbr_render --check-assets                   # decode the assets only (no GPU)
 //
+// Row-partitioned multi-GPU mode (BASELINE config 5; the C++ counterpart of physically_based_renderer_amd/dist.py):
+// one process per GPU, rank / world / local rank from RANK, WORLD_SIZE, LOCAL_RANK (torch.distributed.run
+// --no-python sets them), the RCCL unique id handed from rank 0 to its peers through --rendezvous FILE (a fresh
+// path per job). Each rank fills and shades only its 8-row-aligned band; the bands are gathered into rank 0 by
+// one grouped ncclSend / ncclRecv round per frame (a star over the xGMI links), double-buffered so the gather of
+// frame k overlaps the shading of frame k + 1:
+//   torchrun --nproc-per-node 8 --no-python build/pbr_render --rccl --rendezvous /tmp/id.$$ \
+//            --config 5 --rows-per-rank 1024 --output rgba8 --steps 50
+//   build/pbr_render --print-bands 8 --config 5       # the partition only (no GPU; tests compare it with dist.py)
+//
 // Scenes (same table as physically_based_renderer_amd/scenes.py CONFIGS): 1 rustediron sphere, 1 point light;
 // 2 1920x1080, 8 point lights; 3 3840x2160, 64 point lights + diffuse IBL; 4 3840x2160, 256 point lights,
 // tiled culling, material tiles + F0 plane; 5 8192x8192, 64 point lights + IBL.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -82,9 +95,11 @@ struct Assets {
 
 struct Args {
     int config = 3, width = 0, height = 0, steps = 0, warmup = 3, bands = 1, threads = 0;
+    int rows_per_rank = 0, print_bands = 0;
     double ramp_ms = 200.0;
     std::string output = "rgba32f", mode = "exact", dump, assets = "physically_based_renderer_amd/assets";
-    bool check_assets = false;
+    std::string rendezvous;
+    bool check_assets = false, rccl = false;
 };
 
 Args parse(int argc, char** argv) {
@@ -101,6 +116,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--steps") a.steps = std::stoi(val());
         else if (k == "--warmup") a.warmup = std::stoi(val());
         else if (k == "--bands") a.bands = std::stoi(val());
+        else if (k == "--rows-per-rank") a.rows_per_rank = std::stoi(val());
         else if (k == "--threads") a.threads = std::stoi(val());
         else if (k == "--ramp-ms") a.ramp_ms = std::stod(val());
         else if (k == "--output") a.output = val();
@@ -108,15 +124,279 @@ Args parse(int argc, char** argv) {
         else if (k == "--dump") a.dump = val();
         else if (k == "--assets") a.assets = val();
         else if (k == "--check-assets") a.check_assets = true;
+        else if (k == "--rccl") a.rccl = true;
+        else if (k == "--rendezvous") a.rendezvous = val();
+        else if (k == "--print-bands") a.print_bands = std::stoi(val());
         else throw std::runtime_error("unknown option " + k);
     }
+    if (a.rows_per_rank < 0 || a.print_bands < 0) throw std::runtime_error("--rows-per-rank, --print-bands >= 0");
     if (a.output != "rgba32f" && a.output != "rgba8") throw std::runtime_error("--output rgba32f|rgba8");
     if (a.mode != "exact" && a.mode != "faithful") throw std::runtime_error("--mode exact|faithful");
     if (a.bands < 1) throw std::runtime_error("--bands >= 1");
     return a;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Row-partitioned multi-GPU mode (--rccl).
+
+void throw_if_nccl(ncclResult_t r, const char* expr, const char* file, int line) {
+    if (r != ncclSuccess)
+        throw std::runtime_error(std::string(expr) + " failed in " + file + "; line " + std::to_string(line) +
+                                 "; error: " + ncclGetErrorString(r));
+}
+#define PBR_THROW_IF_NCCL(x) throw_if_nccl((x), #x, __FILE__, __LINE__)
+
+// Rank `rank`'s rows of a `height`-row frame over `world` ranks: equal bands of 8-row shading tiles, the
+// remainder tiles going to the last ranks (physically_based_renderer_amd/dist.py band_rows, align 8).
+struct RowBand {
+    int r0, r1, rows_max;
+    int rows() const { return r1 - r0; }
+};
+
+RowBand band_rows(int height, int world, int rank) {
+    constexpr int kAlign = 8;
+    if (world < 1 || rank < 0 || rank >= world || height < 0) throw std::runtime_error("bad partition");
+    const int tiles = (height + kAlign - 1) / kAlign, per = tiles / world, extra = tiles % world;
+    auto start = [&](int r) { return std::min(height, kAlign * (r * per + std::max(0, r - (world - extra)))); };
+    return {start(rank), start(rank + 1), std::min(height, kAlign * (per + (extra ? 1 : 0)))};
+}
+
+int env_int(const char* name, int fallback) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::atoi(v) : fallback;
+}
+
+// The communicator's unique id, from rank 0 to every peer through a file: written to FILE.tmp and renamed
+// (atomic on one file system), so a peer never reads a partial id; peers poll for it for up to 120 s.
+ncclUniqueId rendezvous(int rank, int world, const std::string& path) {
+    ncclUniqueId id;
+    if (rank == 0) {
+        PBR_THROW_IF_NCCL(ncclGetUniqueId(&id));
+        if (world > 1) {
+            const std::string tmp = path + ".tmp";
+            FILE* f = std::fopen(tmp.c_str(), "wb");
+            if (!f || std::fwrite(&id, sizeof id, 1, f) != 1) throw std::runtime_error("cannot write " + tmp);
+            std::fclose(f);
+            if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot rename " + tmp);
+        }
+        return id;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        if (FILE* f = std::fopen(path.c_str(), "rb")) {
+            const size_t got = std::fread(&id, sizeof id, 1, f);
+            std::fclose(f);
+            if (got == 1) return id;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+            throw std::runtime_error("rank " + std::to_string(rank) + ": no RCCL id in " + path + " after 120 s");
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+}
+
+int run_ranked(const Args& args, const SceneConfig* cfg, Assets& assets) {
+    const int rank = env_int("RANK", 0), world = env_int("WORLD_SIZE", 1), local = env_int("LOCAL_RANK", 0);
+    if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("RANK / WORLD_SIZE out of range");
+    if (world > 1 && args.rendezvous.empty()) throw std::runtime_error("--rccl at WORLD_SIZE > 1 needs --rendezvous FILE");
+    if (args.bands != 1) throw std::runtime_error("--bands is the single-GPU band split; --rccl partitions by rank");
+    // Weak scaling as in bench.py: --rows-per-rank R makes the frame R x world rows (config 5: 1024 x 8 = 8192).
+    const int W = args.width ? args.width : cfg->width;
+    const int H = args.rows_per_rank ? args.rows_per_rank * world : (args.height ? args.height : cfg->height);
+    const RowBand band = band_rows(H, world, rank);
+    const int threads = args.threads ? args.threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    PBR_THROW_IF_HIP(hipSetDevice(local));
+
+    // This rank's rows only: the fill is a function of the global pixel, so the gathered frame equals a
+    // single-GPU frame bit for bit.
+    pbr_scene_desc scene;
+    std::memset(&scene, 0, sizeof scene);
+    scene.kind = cfg->kind;
+    scene.width = W;
+    scene.height = H;
+    scene.seed = cfg->seed;
+    scene.assets = &assets.c;
+    const size_t band_px = static_cast<size_t>(W) * band.rows();
+    std::vector<float> host(pbr::DeviceGBuffer::kPlanes * std::max<size_t>(band_px, 1));
+    float* planes[pbr::DeviceGBuffer::kPlanes];
+    for (int i = 0; i < pbr::DeviceGBuffer::kPlanes; ++i) planes[i] = host.data() + i * band_px;
+    if (band.rows() > 0) PBR_THROW_IF_FAILED(pbr_gbuffer_fill(&scene, band.r0, band.r1, planes, W, threads));
+
+    std::vector<pbr_light> lights(std::max(cfg->n_lights, 1));
+    pbr_pass_desc pass;
+    PBR_THROW_IF_FAILED(pbr_scene_pass(&scene, cfg->n_lights, lights.data(), &pass));
+    pass.ambient_mode = static_cast<int32_t>(cfg->ambient);
+    pass.flags |= cfg->flags;
+    if (args.mode == "faithful") pass.flags |= PBR_FLAG_FAITHFUL;
+
+    hipStream_t shade_stream, comm_stream;
+    PBR_THROW_IF_HIP(hipStreamCreateWithFlags(&shade_stream, hipStreamNonBlocking));
+    PBR_THROW_IF_HIP(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
+    pbr::ShadingContext ctx(local);
+    pbr::DeviceGBuffer gb(W, std::max(band.rows(), 1));
+    if (band.rows() > 0) gb.Upload(host.data(), shade_stream);
+    ctx.SetPass(pass, shade_stream);
+    if (cfg->ambient == pbr::AmbientMode::IblDiffuse)
+        ctx.SetEnvMap(assets.env.texels.data(), assets.env.width, assets.env.height, shade_stream);
+
+    ncclComm_t comm;
+    const ncclUniqueId id = rendezvous(rank, world, args.rendezvous);
+    PBR_THROW_IF_NCCL(ncclCommInitRank(&comm, world, id, rank));
+
+    // Two band slots (rows_max rows, the gather's fixed message size) so frame k + 1 shades while frame k is in
+    // flight; rank 0 also holds the (world, rows_max, W) gather buffer.
+    const bool rgba8 = args.output == "rgba8";
+    const size_t px_bytes = rgba8 ? 4 : 16, slot_bytes = px_bytes * W * static_cast<size_t>(band.rows_max);
+    const pbr_output_format fmt = rgba8 ? PBR_OUTPUT_RGBA8_UNORM : PBR_OUTPUT_RGBA32F;
+    void* slots[2];
+    for (auto& s : slots) {
+        PBR_THROW_IF_HIP(hipMalloc(&s, std::max<size_t>(slot_bytes, 1)));
+        PBR_THROW_IF_HIP(hipMemsetAsync(s, 0, slot_bytes, shade_stream));
+    }
+    uint8_t* frame = nullptr;
+    if (rank == 0) PBR_THROW_IF_HIP(hipMalloc(reinterpret_cast<void**>(&frame), std::max<size_t>(slot_bytes * world, 1)));
+    hipEvent_t shaded[2], gathered[2];
+    for (int i = 0; i < 2; ++i) {
+        PBR_THROW_IF_HIP(hipEventCreateWithFlags(&shaded[i], hipEventDisableTiming));
+        PBR_THROW_IF_HIP(hipEventCreateWithFlags(&gathered[i], hipEventDisableTiming));
+        PBR_THROW_IF_HIP(hipEventRecord(gathered[i], comm_stream));
+    }
+
+    // One grouped round: every peer sends its slot straight to rank 0 over its own link; rank 0 copies its own
+    // band and posts one receive per peer (dist.BandGather.start).
+    auto gather = [&](int slot) {
+        PBR_THROW_IF_NCCL(ncclGroupStart());
+        if (rank == 0) {
+            PBR_THROW_IF_HIP(hipMemcpyAsync(frame, slots[slot], slot_bytes, hipMemcpyDeviceToDevice, comm_stream));
+            for (int r = 1; r < world; ++r)
+                PBR_THROW_IF_NCCL(ncclRecv(frame + slot_bytes * r, slot_bytes, ncclUint8, r, comm, comm_stream));
+        } else {
+            PBR_THROW_IF_NCCL(ncclSend(slots[slot], slot_bytes, ncclUint8, 0, comm, comm_stream));
+        }
+        PBR_THROW_IF_NCCL(ncclGroupEnd());
+    };
+    auto step = [&](int k, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+        const int slot = k & 1;
+        PBR_THROW_IF_HIP(hipStreamWaitEvent(shade_stream, gathered[slot], 0));  // the gather that last read it
+        if (ev0) PBR_THROW_IF_HIP(hipEventRecord(ev0, shade_stream));
+        if (band.rows() > 0) ctx.ShadeFrame(gb.Band(0, band.rows()), slots[slot], W, fmt, nullptr, 0, shade_stream);
+        if (ev1) PBR_THROW_IF_HIP(hipEventRecord(ev1, shade_stream));
+        PBR_THROW_IF_HIP(hipEventRecord(shaded[slot], shade_stream));
+        PBR_THROW_IF_HIP(hipStreamWaitEvent(comm_stream, shaded[slot], 0));
+        gather(slot);
+        PBR_THROW_IF_HIP(hipEventRecord(gathered[slot], comm_stream));
+    };
+    // Barrier + reduction over ranks on the device (RCCL all-reduce of one value, then host sync).
+    double* d_red = nullptr;
+    PBR_THROW_IF_HIP(hipMalloc(reinterpret_cast<void**>(&d_red), sizeof(double)));
+    auto reduce = [&](double v, ncclRedOp_t op) {
+        PBR_THROW_IF_HIP(hipStreamSynchronize(shade_stream));
+        PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+        PBR_THROW_IF_HIP(hipMemcpyAsync(d_red, &v, sizeof v, hipMemcpyHostToDevice, comm_stream));
+        PBR_THROW_IF_NCCL(ncclAllReduce(d_red, d_red, 1, ncclFloat64, op, comm, comm_stream));
+        PBR_THROW_IF_HIP(hipMemcpyAsync(&v, d_red, sizeof v, hipMemcpyDeviceToHost, comm_stream));
+        PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+        return v;
+    };
+    reduce(0.0, ncclSum);  // every rank has joined (and uploaded) before anything is timed
+    if (rank == 0 && world > 1) std::remove(args.rendezvous.c_str());
+
+    if (args.steps <= 0) {
+        step(0);
+        reduce(0.0, ncclSum);
+        if (rank == 0) {  // stitch the bands' rows (slots are rows_max tall; the tail bands may be shorter)
+            std::vector<uint8_t> slotted(slot_bytes * world), image;
+            PBR_THROW_IF_HIP(hipMemcpy(slotted.data(), frame, slotted.size(), hipMemcpyDeviceToHost));
+            image.reserve(px_bytes * W * static_cast<size_t>(H));
+            for (int r = 0; r < world; ++r) {
+                const uint8_t* s = slotted.data() + slot_bytes * r;
+                image.insert(image.end(), s, s + px_bytes * W * static_cast<size_t>(band_rows(H, world, r).rows()));
+            }
+            if (!args.dump.empty()) {
+                FILE* f = std::fopen(args.dump.c_str(), "wb");
+                if (!f) throw std::runtime_error("cannot write " + args.dump);
+                const int32_t hdr[4] = {W, H, static_cast<int32_t>(px_bytes), 0};
+                std::fwrite(hdr, sizeof hdr, 1, f);
+                std::fwrite(image.data(), 1, image.size(), f);
+                std::fclose(f);
+            }
+            std::printf("{\"tool\": \"pbr_render\", \"workload\": \"%s\", \"width\": %d, \"height\": %d, \"world\": %d, "
+                        "\"rows_per_rank\": %d, \"output\": \"%s\", \"mode\": \"%s\", \"process_group\": \"rccl\", "
+                        "\"fnv1a\": \"%016llx\"}\n",
+                        cfg->name, W, H, world, band.rows_max, args.output.c_str(), args.mode.c_str(),
+                        (unsigned long long)fnv1a(image.data(), image.size()));
+        }
+    } else {
+        const auto tr = std::chrono::steady_clock::now();
+        int ramp = 0;
+        while (args.ramp_ms > 0) {  // clock ramp, untimed (bench.py --ramp-ms)
+            step(ramp++);
+            if (ramp % 8 == 0) {
+                PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+                if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count() >= args.ramp_ms) break;
+            }
+        }
+        for (int i = 0; i < args.warmup; ++i) step(i);
+        std::vector<hipEvent_t> ev(2 * args.steps);
+        for (auto& e : ev) PBR_THROW_IF_HIP(hipEventCreate(&e));
+        reduce(0.0, ncclSum);
+        const auto ts = std::chrono::steady_clock::now();
+        for (int i = 0; i < args.steps; ++i) step(i, ev[2 * i], ev[2 * i + 1]);
+        PBR_THROW_IF_HIP(hipStreamSynchronize(shade_stream));
+        PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+        const double wall = reduce(std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count(), ncclMax);
+        double shade_ms = 0;
+        for (int i = 0; i < args.steps; ++i) {
+            float ms = 0;
+            PBR_THROW_IF_HIP(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+            shade_ms += ms;
+        }
+        shade_ms = reduce(shade_ms / args.steps, ncclMax);
+        for (auto& e : ev) (void)hipEventDestroy(e);
+        // The gather alone, timed the same way: the exchange the pipelined step hides behind the shading.
+        reduce(0.0, ncclSum);
+        const auto tg = std::chrono::steady_clock::now();
+        for (int i = 0; i < args.steps; ++i) gather(i & 1);
+        PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+        const double gather_wall = reduce(std::chrono::duration<double>(std::chrono::steady_clock::now() - tg).count(), ncclMax);
+        if (rank == 0)
+            std::printf("{\"tool\": \"pbr_render\", \"workload\": \"%s\", \"width\": %d, \"height\": %d, \"world\": %d, "
+                        "\"rows_per_rank\": %d, \"output\": \"%s\", \"mode\": \"%s\", \"process_group\": \"rccl\", "
+                        "\"steps\": %d, \"value\": %.2f, \"unit\": \"Mpix/s\", \"scaling\": \"weak\", \"ms_per_step\": %.4f, "
+                        "\"shade_ms\": %.4f, \"gather_ms\": %.4f, \"clock_ramp_launches\": %d}\n",
+                        cfg->name, W, H, world, band.rows_max, args.output.c_str(), args.mode.c_str(), args.steps,
+                        static_cast<double>(W) * H * args.steps / wall / 1e6, wall / args.steps * 1e3, shade_ms,
+                        gather_wall / args.steps * 1e3, ramp);
+    }
+    PBR_THROW_IF_HIP(hipStreamSynchronize(shade_stream));
+    PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+    PBR_THROW_IF_NCCL(ncclCommDestroy(comm));
+    for (int i = 0; i < 2; ++i) {
+        (void)hipEventDestroy(shaded[i]);
+        (void)hipEventDestroy(gathered[i]);
+        PBR_THROW_IF_HIP(hipFree(slots[i]));
+    }
+    if (frame) PBR_THROW_IF_HIP(hipFree(frame));
+    PBR_THROW_IF_HIP(hipFree(d_red));
+    PBR_THROW_IF_HIP(hipStreamDestroy(shade_stream));
+    PBR_THROW_IF_HIP(hipStreamDestroy(comm_stream));
+    return 0;
+}
+
 int run(const Args& args) {
+    if (args.print_bands) {  // the rank partition only (no assets, no GPU)
+        const SceneConfig* c = nullptr;
+        for (const auto& k : kConfigs)
+            if (k.id == args.config) c = &k;
+        if (!c) throw std::runtime_error("--config 1..5");
+        const int H = args.rows_per_rank ? args.rows_per_rank * args.print_bands : (args.height ? args.height : c->height);
+        std::printf("[");
+        for (int r = 0; r < args.print_bands; ++r) {
+            const RowBand b = band_rows(H, args.print_bands, r);
+            std::printf("%s[%d, %d, %d]", r ? ", " : "", b.r0, b.r1, b.rows_max);
+        }
+        std::printf("]\n");
+        return 0;
+    }
     Assets assets(args.assets);
     if (args.check_assets) {  // decode only: checksums the CPU test compares with numpy's decode
         for (const auto& set : {std::make_pair("rustediron_256", &assets.rust), std::make_pair("materials_1k_64", &assets.mats)})
@@ -132,6 +412,8 @@ int run(const Args& args) {
     for (const auto& c : kConfigs)
         if (c.id == args.config) cfg = &c;
     if (!cfg) throw std::runtime_error("--config 1..5");
+    if (args.rccl) return run_ranked(args, cfg, assets);
+    if (args.rows_per_rank) throw std::runtime_error("--rows-per-rank needs --rccl (or --print-bands)");
     const int W = args.width ? args.width : cfg->width, H = args.height ? args.height : cfg->height;
     const int threads = args.threads ? args.threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 

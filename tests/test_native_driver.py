@@ -32,7 +32,7 @@ def driver(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("native") / "pbr_render")
     lib_dir = os.path.dirname(N.LIB_PATH)
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I",
-           os.path.join(ROOT, "include"), SRC, "-L", lib_dir, "-lpbrshade", "-lz", f"-Wl,-rpath,{lib_dir}", "-o", exe]
+           os.path.join(ROOT, "include"), SRC, "-L", lib_dir, "-lpbrshade", "-lrccl", "-lz", f"-Wl,-rpath,{lib_dir}", "-o", exe]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     return exe
@@ -54,6 +54,28 @@ def test_asset_decoders_match_numpy(driver):
             assert got[f"{npz}/{k}"] == fnv1a(np.ascontiguousarray(arrs[k], np.uint8).tobytes()), k
     env = envmap.load_chelsea_stairs_env()
     assert got[f"env {env.shape[1]}x{env.shape[0]}"] == fnv1a(env.tobytes())
+
+
+@pytest.mark.parametrize("height,world,rows_per_rank", [(8192, 8, 1024), (203, 3, 0), (203, 8, 0), (64, 1, 64),
+                                                        (17, 4, 0), (4096, 5, 0)])
+def test_rank_partition_equals_dist_band_rows(driver, height, world, rows_per_rank):
+    """The native --rccl mode's row bands are dist.band_rows' (8-row tiles, remainder to the last ranks)."""
+    from physically_based_renderer_amd import dist as D
+
+    args = ["--print-bands", world, "--config", 5]
+    args += ["--rows-per-rank", rows_per_rank] if rows_per_rank else ["--height", height]
+    r = run(driver, *args)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    want = [[b.row_begin, b.row_end, b.rows_max] for b in D.all_bands(height, world)]
+    assert got == want
+
+
+def test_rccl_mode_argument_errors(driver):
+    r = run(driver, "--rccl", "--config", "5", "--bands", "2")
+    assert r.returncode == 2 and "--bands" in r.stderr
+    r = run(driver, "--config", "5", "--rows-per-rank", "64")
+    assert r.returncode == 2 and "--rccl" in r.stderr
 
 
 def test_errors_are_reported_like_throw_if_failed(driver):
@@ -123,4 +145,50 @@ def test_native_timed_run(driver, gpu, mode):
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["steps"] == 10 and d["value"] > 1000.0  # north-star floor: 10^9 shaded px/s
+    print(d)
+
+
+def _torchrun_native(driver, nproc, *args, timeout=300):
+    import socket
+    import sys
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "--no-python", driver, *map(str, args)]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("output", ["rgba8", "rgba32f"])
+def test_native_rccl_frame_equals_single_gpu_frame(driver, tmp_path, gpu, output):
+    """--rccl under torch.distributed.run (one rank: the RCCL communicator init, the grouped send/recv gather round,
+    the all-reduce barrier and teardown all run): the assembled config-5 frame is byte-equal to the same frame shaded
+    by the single-process pbr_shade_frame path."""
+    ranked, whole = str(tmp_path / "ranked.bin"), str(tmp_path / "whole.bin")
+    r = _torchrun_native(driver, 1, "--rccl", "--rendezvous", str(tmp_path / "id"), "--config", 5, "--width", 1024,
+                         "--rows-per-rank", 96, "--output", output, "--mode", "faithful", "--dump", ranked)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["process_group"] == "rccl" and line["world"] == 1 and line["height"] == 96
+    r = run(driver, "--config", 5, "--width", 1024, "--height", 96, "--output", output, "--mode", "faithful",
+            "--dump", whole)
+    assert r.returncode == 0, r.stderr
+    a, b = open(ranked, "rb").read(), open(whole, "rb").read()
+    assert len(a) == len(b) == 16 + 1024 * 96 * (4 if output == "rgba8" else 16)
+    assert a == b
+
+
+@pytest.mark.gpu
+def test_native_rccl_timed_run(driver, tmp_path, gpu):
+    """The timed --rccl step (shade on one stream, gather on another, double-buffered): one JSON line from rank 0 with
+    the max-over-ranks wall clock and the shade / gather split, per-rank band of config 5's 8192 x 1024 geometry."""
+    r = _torchrun_native(driver, 1, "--rccl", "--rendezvous", str(tmp_path / "id"), "--config", 5,
+                         "--rows-per-rank", 1024, "--output", "rgba8", "--mode", "faithful", "--steps", 10,
+                         "--warmup", 2, "--ramp-ms", 50)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["width"] == 8192 and d["height"] == 1024 and d["rows_per_rank"] == 1024 and d["steps"] == 10
+    assert d["value"] > 1000.0 and d["shade_ms"] > 0 and d["gather_ms"] > 0 and d["scaling"] == "weak"
     print(d)
