@@ -558,10 +558,11 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
         if (active) {
             const int j0 = __builtin_ctzll(m);
             m &= m - 1;
-            const bool two = m != 0;
-            const int j1 = two ? __builtin_ctzll(m) : j0;  // one light left: the second element repeats it ...
-            m &= two ? m - 1 : m;
-            const int s1 = two ? j1 : kBalMaxLights;         // ... with the zero strength: it adds +0
+            // One light left: the second element's strength is the zero sentinel (index kBalMaxLights) and its
+            // position repeats the first element's light, so it adds +0 and passes the same window tests.
+            const int s1 = m != 0 ? __builtin_ctzll(m) : kBalMaxLights;
+            m &= m - 1;  // no-op when m == 0
+            const int j1 = s1 == kBalMaxLights ? j0 : s1;
             m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests; only this lane's bits are read
             f3x2 lp, ls;
             read_pair_lights(lds_lights, j0, j1, s1, lp, ls);
