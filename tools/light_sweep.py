@@ -56,6 +56,24 @@ def main():
             slope = "" if prev is None else f"  +{(ms - prev[1]) / (n - prev[0]) * 1e6 / px * 1e3:.3f} ps/px/light"
             print(f"lights {n:3d}: {ms:.4f} ms  {px / ms / 1e3:9.1f} Mpix/s{slope}", flush=True)
             prev = (n, ms)
+        # Memory floor for the same bytes: read the 11 planes the constant-ambient pass reads (sum over planes,
+        # 44 B/px in, 4 B/px out) and write the 16 B/px RGBA output (fill), each timed alone.
+        def timed(fn):
+            for _ in range(3):
+                fn()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+            for e0, e1 in ev:
+                e0.record()
+                fn()
+                e1.record()
+            torch.cuda.synchronize()
+            return float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+        src = gb.planes[:11]
+        acc = torch.empty((a.height, a.width), device=dev)
+        t_rd = timed(lambda: torch.sum(src, dim=0, out=acc))
+        t_wr = timed(lambda: out.fill_(0.5))
+        print(f"memory floor: read 11 planes {t_rd:.4f} ms ({44 * px / t_rd / 1e6:.0f} GB/s), write RGBA "
+              f"{t_wr:.4f} ms ({16 * px / t_wr / 1e6:.0f} GB/s), sum {t_rd + t_wr:.4f} ms", flush=True)
 
 
 if __name__ == "__main__":
