@@ -51,8 +51,9 @@ struct pbr_context {
     int64_t last_slots = 0;  // statistics records of the last pass (shade_stat_slots_per_tile per tile)
     bool last_culled = false;
     // Wave-balanced point-light lists (pbr_balanced.h) for untiled passes with at least this many point lights
-    // and no spot lights; PBR_BALANCED_MIN overrides (0 disables).
-    int balanced_min = 16;
+    // and no spot lights; -1: the measured crossover of the mode (kBalancedMinFaithful / kBalancedMinExact);
+    // PBR_BALANCED_MIN overrides both (0 disables).
+    int balanced_min = -1;
     bool points_flag_ok = false;  // pbr_set_pass: every point light inside the fast-path window
     int pixels_per_thread = 2;  // kernel layout: packed pixel pairs (measured faster); PBR_PIXELS_PER_THREAD=1 overrides
     std::string last_error;
@@ -368,8 +369,14 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     // Wave-balanced point-light lists: untiled pair-kernel passes with no spot lights, every point light inside
     // the fast-path window; faithful (1) or exact (2, and no directional lights either) -- the exact variant
     // keeps the reference's order per pixel (bit-identical), the faithful one re-associates.
-    const bool bal_ok = !cull && a.pixels_per_thread == 2 && ctx->balanced_min > 0 && ctx->points_flag_ok &&
-                        a.ps.n_spot == 0 && a.ps.n_point >= ctx->balanced_min && a.ps.n_point <= pbr::kBalMaxLights;
+    // Point-light count from which the balanced lists win (same-box sweeps, 1080p and 4K): the
+    // faithful loop between 20 (uniform faster) and 24 lights, the exact loop between 16 and 20.
+    constexpr int kBalancedMinFaithful = 22, kBalancedMinExact = 18;
+    const int bal_min = ctx->balanced_min >= 0 ? ctx->balanced_min
+                        : a.ps.faithful == 1   ? kBalancedMinFaithful
+                                               : kBalancedMinExact;
+    const bool bal_ok = !cull && a.pixels_per_thread == 2 && bal_min > 0 && ctx->points_flag_ok &&
+                        a.ps.n_spot == 0 && a.ps.n_point >= bal_min && a.ps.n_point <= pbr::kBalMaxLights;
     a.ps.balanced = !bal_ok                                                ? 0
                     : a.ps.faithful == 1                                   ? 1
                     : a.ps.faithful == 0 && !a.exact_only && a.ps.n_dir == 0 ? 2

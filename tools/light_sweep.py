@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--ibl", action="store_true")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--flags", type=int, default=0, help="extra pass flags, e.g. 16 = PBR_FLAG_FAITHFUL")
+    ap.add_argument("--counts", type=int, nargs="+", default=[0, 1, 2, 4, 8, 16, 32, 64])
+    ap.add_argument("--no-floor", action="store_true")
     a = ap.parse_args()
     cfg = S.CONFIGS[3].with_size(a.width, a.height)
     planes, _ = S.fill_gbuffer_host(cfg)
@@ -39,7 +41,7 @@ def main():
         ctx.set_pass(base)
         clock_ramp(ctx, gb, out)
         prev = None
-        for n in (0, 1, 2, 4, 8, 16, 32, 64):
+        for n in a.counts:
             pc = PassConstants(eye_pos_w=base.eye_pos_w, num_point_lights=n, lights_array=lights[:max(n, 1)],
                                ambient_mode=N.PBR_AMBIENT_IBL_DIFFUSE if a.ibl else N.PBR_AMBIENT_CONSTANT,
                                flags=a.flags)
@@ -68,6 +70,8 @@ def main():
                 e1.record()
             torch.cuda.synchronize()
             return float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+        if a.no_floor:
+            return
         src = gb.planes[:11]
         acc = torch.empty((a.height, a.width), device=dev)
         t_rd = timed(lambda: torch.sum(src, dim=0, out=acc))
