@@ -239,3 +239,37 @@ def test_balanced_light_outside_window_sends_all_to_exact(ctx_pair, gpu):
     want, redo_p = run(plain, gb, pc)
     assert redo_b == redo_p == 128 * 4
     assert close(got, want)
+
+
+@pytest.fixture(scope="module")
+def ctx_default(gpu):
+    """A context with the built-in per-mode minimums (PBR_BALANCED_MIN unset)."""
+    import os
+
+    old = os.environ.pop("PBR_BALANCED_MIN", None)
+    ctx = ShadingContext(0)
+    if old is not None:
+        os.environ["PBR_BALANCED_MIN"] = old
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("mode,n_lights", [("faithful", 21), ("faithful", 22), ("exact", 17), ("exact", 18)])
+def test_default_balancing_minimum(mode, n_lights, ctx_default, ctx_pair, gpu):
+    """The built-in minimums (faithful 22, exact 18 point lights; pbr_context.hip): one light below a minimum
+    the default context runs the uniform loop (its frame has the uniform kernel's bits), at the minimum it
+    runs the balanced lists; both match the oracle at the mode's bar."""
+    rng = np.random.default_rng(500 + n_lights)
+    planes, lights = _scene(rng, 256, 8, n_lights)
+    flags = N.PBR_FLAG_FAITHFUL if mode == "faithful" else 0
+    pc = PassConstants(num_point_lights=n_lights, lights_array=lights, flags=flags)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, _ = run(ctx_default, gb, pc)
+    want_plain, _ = run(plain, gb, pc)
+    want_bal, _ = run(bal, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    minimum = 22 if mode == "faithful" else 18
+    expect = want_bal if n_lights >= minimum else want_plain
+    assert O.bit_equal(got, expect).all()
+    check_mode(mode, got, want_plain, ref)
