@@ -395,7 +395,7 @@ __device__ __forceinline__ void launder(f3x2& x) {
     launder(x.y);
     launder(x.z);
 }
-__device__ __forceinline__ void launder(PairIn& p) {
+[[maybe_unused]] __device__ __forceinline__ void launder(PairIn& p) {
     launder(p.pos);
     launder(p.n);
     launder(p.albedo);
@@ -870,6 +870,76 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
                          : sky_pixel(q.n, ps, fr.sky, !exact_only));
 }
 
+// The balanced-list kernels (BAL 1, 2) are compiled in their own translation unit, shade_kernels_bal.hip,
+// which includes this file with PBR_BAL_TU defined: the Makefile builds this one with the max-ILP machine
+// scheduler (faster for the uniform and culled loops, no scratch) and that one with the default scheduler
+// (max-ILP spills 12-44 B/lane in the balanced kernels). Profiling builds (PBR_BAL_PROFILE) keep everything
+// here, so that one g_bal_prof_buf collects every kernel's stamps.
+#if defined(PBR_BAL_PROFILE) && PBR_BAL_PROFILE
+#define PBR_SPLIT_BAL 0
+#else
+#define PBR_SPLIT_BAL 1
+#endif
+#ifndef PBR_BAL_TU
+#define PBR_BAL_TU 0
+#endif
+
+// Launches the balanced variant (a.ps.balanced 1 or 2) of shade_tile_kernel over `grid`.
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO>
+hipError_t launch_balanced(const LaunchArgs& a, dim3 grid, hipStream_t stream);
+
+#if PBR_BAL_TU == PBR_SPLIT_BAL
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO>
+hipError_t launch_balanced(const LaunchArgs& a, dim3 grid, hipStream_t stream) {
+    if (a.ps.balanced == 1)
+        hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 1>), grid, dim3(kBlock), 0, stream,
+                           a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
+    else
+        hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 2>), grid, dim3(kBlock), 0, stream,
+                           a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
+    return hipGetLastError();
+}
+#define PBR_INSTANTIATE_BAL(A, F, O) template hipError_t launch_balanced<A, F, O>(const LaunchArgs&, dim3, hipStream_t);
+PBR_INSTANTIATE_BAL(kAmbientConstant, false, false)
+PBR_INSTANTIATE_BAL(kAmbientConstant, false, true)
+PBR_INSTANTIATE_BAL(kAmbientConstant, true, false)
+PBR_INSTANTIATE_BAL(kAmbientConstant, true, true)
+PBR_INSTANTIATE_BAL(kAmbientIblDiffuse, false, false)
+PBR_INSTANTIATE_BAL(kAmbientIblDiffuse, false, true)
+PBR_INSTANTIATE_BAL(kAmbientIblDiffuse, true, false)
+PBR_INSTANTIATE_BAL(kAmbientIblDiffuse, true, true)
+#undef PBR_INSTANTIATE_BAL
+
+// Development builds with PBR_BAL_PROFILE: read (and optionally clear) the balanced pass's clock sums.
+hipError_t debug_bal_profile(unsigned long long* out8, bool reset) {
+#if PBR_BAL_PROFILE
+    constexpr size_t kWaves = 1 << 18, kBytes = kWaves * 16 * sizeof(unsigned long long);
+    static unsigned long long* buf = nullptr;
+    hipError_t e = hipSuccess;
+    if (!buf) {
+        e = hipMalloc(&buf, kBytes);
+        if (e == hipSuccess) e = hipMemset(buf, 0, kBytes);
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_bal_prof_buf), &buf, sizeof(buf));
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
+    std::vector<unsigned long long> h(kWaves * 16);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), buf, kBytes, hipMemcpyDeviceToHost);
+    for (int i = 0; i < 16; ++i) out8[i] = 0;
+    for (size_t w = 0; w < kWaves; ++w)
+        for (int i = 0; i < 16; ++i) out8[i] += h[w * 16 + i];
+    if (e == hipSuccess && reset) e = hipMemset(buf, 0, kBytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return e;
+#else
+    (void)out8;
+    (void)reset;
+    return hipErrorNotSupported;
+#endif
+}
+
+#endif
+
+#if !PBR_BAL_TU
 __global__ void decode_unorm16_kernel(const uint16_t* __restrict__ src, float4* __restrict__ dst, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
@@ -883,12 +953,8 @@ template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL>
 static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
     if (a.pixels_per_thread == 2) {
         dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
-        if (!CULL && a.ps.balanced == 1)
-            hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 1>), grid, dim3(kBlock), 0,
-                               stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
-        else if (!CULL && a.ps.balanced == 2)
-            hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 2>), grid, dim3(kBlock), 0,
-                               stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
+        if (!CULL && a.ps.balanced != 0)
+            return launch_balanced<AMBIENT, F0_PLANE, APPLY_AO>(a, grid, stream);
         else
             hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,
                                a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
@@ -927,37 +993,12 @@ int64_t shade_tile_count(int width, int height, int pixels_per_thread) {
 
 int shade_stat_slots_per_tile(int pixels_per_thread) { return pixels_per_thread == 2 ? kBlock / 64 : 1; }
 
-// Development builds with PBR_BAL_PROFILE: read (and optionally clear) the balanced pass's clock sums.
-hipError_t debug_bal_profile(unsigned long long* out8, bool reset) {
-#if PBR_BAL_PROFILE
-    constexpr size_t kWaves = 1 << 18, kBytes = kWaves * 16 * sizeof(unsigned long long);
-    static unsigned long long* buf = nullptr;
-    hipError_t e = hipSuccess;
-    if (!buf) {
-        e = hipMalloc(&buf, kBytes);
-        if (e == hipSuccess) e = hipMemset(buf, 0, kBytes);
-        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_bal_prof_buf), &buf, sizeof(buf));
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-    }
-    std::vector<unsigned long long> h(kWaves * 16);
-    if (e == hipSuccess) e = hipMemcpy(h.data(), buf, kBytes, hipMemcpyDeviceToHost);
-    for (int i = 0; i < 16; ++i) out8[i] = 0;
-    for (size_t w = 0; w < kWaves; ++w)
-        for (int i = 0; i < 16; ++i) out8[i] += h[w * 16 + i];
-    if (e == hipSuccess && reset) e = hipMemset(buf, 0, kBytes);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    return e;
-#else
-    (void)out8;
-    (void)reset;
-    return hipErrorNotSupported;
-#endif
-}
-
 hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream) {
     if (n_texels <= 0) return hipSuccess;
     hipLaunchKernelGGL(decode_unorm16_kernel, dim3((n_texels + 255) / 256), dim3(256), 0, stream, src, dst, n_texels);
     return hipGetLastError();
 }
+
+#endif  // !PBR_BAL_TU
 
 }  // namespace pbr
