@@ -59,35 +59,65 @@ def bytes_per_pixel(pc, out_bytes: int = 16) -> int:
     return planes * 4 + out_bytes
 
 
+FLOP_DIR = FLOP_POINT - 17  # 74 per directional light (no distance / attenuation)
+FLOP_BACKFACE_TEST = 8  # the wave-balanced lists' pass-1 test: 4 FMAs per (pixel, point light)
+
+
 def flops_per_pixel(pc, lights_per_tile=None, tile_px: int = 128) -> float:
-    """Algorithmic FLOP per pixel. With tiled culling only the lights that survive a tile are shaded
-    (base + L_in per-light BRDFs); the 9-FLOP range test of every point/spot light is
-    counted once per culling tile (the unit that runs it), not per pixel, so skipped work is never counted."""
+    """Algorithmic FLOP per pixel, SURVEY 8(d)'s model: every light of the pass for every pixel
+    (LightingUtil.hlsl:176-199 sums them all). With tiled culling only the lights that survive a tile are
+    shaded (base + L_in per-light BRDFs); the 9-FLOP range test of every point/spot light is
+    counted once per culling tile (the unit that runs it), not per pixel."""
     n_ps = pc.num_point_lights + pc.num_spot_lights
     f = FLOP_BASE + FLOP_HOIST
     if pc.flags & N.PBR_FLAG_TILED_CULLING and lights_per_tile is not None:
         f += FLOP_POINT * lights_per_tile + FLOP_RANGE_TEST * n_ps / tile_px
     else:
         f += FLOP_POINT * n_ps
-    f += (FLOP_POINT - 17) * pc.num_dir_lights  # 74 per directional light (no distance/attenuation)
+    f += FLOP_DIR * pc.num_dir_lights
     if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE:
         f += FLOP_IBL
     return round(f, 2)
 
 
-def load_pmc(workload: str):
-    """(HBM bytes per launch, VALU-issue busy fraction) from the committed rocprofv3 PMC summary of
-    this workload (profiles/pmc_summary.json, tools/pmc_summarize.py), or (None, None)."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def executed_flops_per_pixel(pc, st: dict, px: int) -> float:
+    """FLOP per pixel of the work the pass executed, from its own statistics (pbr_last_pass_stats): the
+    per-pixel part for every geometry pixel, 91 / 74 FLOP per point / directional light term the light loops
+    evaluated (the wave-balanced lists skip back-facing terms, tiled culling skips out-of-range lights: neither
+    is credited), the lists' back-face tests and the culling range tests. Skipped work is never counted."""
+    geo = st["geometry_pixels"]
+    dir_terms = pc.num_dir_lights * geo
+    f = (FLOP_BASE + FLOP_HOIST + (FLOP_IBL if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else 0)) * geo
+    f += FLOP_POINT * (st["light_terms"] - dir_terms) + FLOP_DIR * dir_terms
+    f += FLOP_BACKFACE_TEST * st["backface_tests"]
+    if st["culled"]:
+        f += FLOP_RANGE_TEST * (pc.num_point_lights + pc.num_spot_lights) * st["cull_tiles"]
+    return round(f / max(px, 1), 2)
+
+
+def load_pmc(workload: str, path: str = os.path.join(ROOT, "profiles", "pmc_summary.json")):
+    """(HBM bytes per launch, VALU-issue busy fraction, provenance) from the committed rocprofv3 PMC summary of
+    this workload (profiles/pmc_summary.json, tools/pmc_summarize.py). The counters are quoted only when the
+    summary's kernel_sources_sha equals the hash of the kernel sources this run is built from; otherwise
+    (a kernel changed since the profile, or an unstamped profile) they are None and the provenance says so."""
+    head = N.kernel_sources_sha()
     try:
         with open(path) as f:
             e = json.load(f).get(workload)
-        if e is None:
-            return None, None
+    except (OSError, ValueError):
+        e = None
+    if e is None:
+        return None, None, {"profile": None, "kernel_sources_sha": head}
+    prov = {"profile": e.get("source"), "profile_kernel_sources_sha": e.get("kernel_sources_sha"),
+            "kernel_sources_sha": head, "profile_revision": e.get("kernel_revision")}
+    if e.get("kernel_sources_sha") != head:
+        prov["stale"] = True
+        return None, None, prov
+    try:
         busy = e.get("valu_issue_busy")
-        return float(e["hbm_bytes_per_launch"]), (None if busy is None else round(float(busy), 3))
-    except (OSError, ValueError, KeyError, TypeError):
-        return None, None
+        return float(e["hbm_bytes_per_launch"]), (None if busy is None else round(float(busy), 3)), prov
+    except (KeyError, TypeError, ValueError):
+        return None, None, prov
 
 
 def host_cpu_budget() -> dict:
@@ -243,6 +273,92 @@ def time_exact_mode(ctx, pc, gb, out, stream, args, fmt, rgba8, px):
             "avg_launch_ms": round(float(np.mean(ms)), 4), "median_launch_ms": round(float(np.median(ms)), 4)}
 
 
+def make_workload(cfg, band, mode: str, device):
+    """The pass constants, env map and resident G-buffer rows of `band` of frame `cfg` (host fill into
+    pinned staging, one upload). Returns (pc, env, staging, gb, fill_s, upload_s)."""
+    from physically_based_renderer_amd.renderer import GBuffer
+
+    t0 = time.perf_counter()
+    pc = S.scene_pass(cfg)
+    if mode == "faithful":
+        pc.flags = int(pc.flags) | N.PBR_FLAG_FAITHFUL
+    env = S.env_map() if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
+    staging = torch.empty((N.NUM_PLANES, band.rows, cfg.width), dtype=torch.float32, pin_memory=True)
+    S.fill_gbuffer_host(cfg, band.row_begin, band.row_end, out=staging.numpy())
+    t_fill = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    planes_dev = staging.to(device, non_blocking=True)
+    torch.cuda.synchronize()
+    return pc, env, staging, GBuffer(planes_dev), t_fill, time.perf_counter() - t1
+
+
+def shade_steps(shade_into, outs, stream, warmup: int, steps: int, gather=None, in_group=False):
+    """W untimed warm-up steps, then exactly K timed steps between barrier + synchronize on both sides. A
+    step shades into one of two output slots; with `gather`, the slot is then gathered to rank 0 (pipelined:
+    the gather of frame k overlaps the shading of frame k + 1; a slot is reused only after its gather).
+    Each shading launch is bracketed by HIP events on the launch stream. Returns (wall s, [launch ms])."""
+    pending = [[], []]
+
+    def step(k: int, ev=None):
+        slot = k % 2
+        D.BandGather.wait(pending[slot])  # the gather that last read this slot (stream-side wait)
+        if ev is not None:
+            ev[0].record(stream)
+        shade_into(outs[slot])
+        if ev is not None:
+            ev[1].record(stream)
+        if gather is not None:
+            pending[slot] = gather.start(outs[slot])
+
+    for k in range(warmup):
+        step(k)
+    for p in pending:
+        D.BandGather.wait(p)
+    pending = [[], []]
+    torch.cuda.synchronize()
+    if in_group:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t_start = time.perf_counter()
+    for k in range(steps):
+        step(k, events[k])
+    for p in pending:
+        D.BandGather.wait(p)
+    torch.cuda.synchronize()
+    if in_group:
+        dist.barrier()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t_start, [a.elapsed_time(b) for a, b in events]
+
+
+def band_anchor(ctx, args, world: int, device, stream, resident=None) -> dict:
+    """The scaling anchor: ONE rank's config-5 band (8192 x rows_per_rank, RGBA8, the run's mode) shaded alone
+    -- no gather, no other rank -- timed like a step. It is the per-GPU work of every point of the 1/2/4/8-GPU
+    curve, so `efficiency_vs_anchor` = (value / N) / anchor compares identical per-rank geometry. At N > 1 the
+    rank's own resident band (`resident` = (gb, outs)); at N = 1 (headline config 3) the band is built here."""
+    rows = args.rows_per_rank
+    cfg5 = S.CONFIGS[5].with_size(8192, rows * world)
+    if resident is None:
+        pc5, env5, _, gb, _, _ = make_workload(cfg5, D.band_rows(rows, 1, 0), args.mode, device)
+        ctx.set_pass(pc5, stream)
+        if env5 is not None:
+            ctx.set_env_map(env5, stream)
+        outs = [torch.empty((rows, cfg5.width, 4), dtype=torch.uint8, device=device) for _ in range(2)]
+    else:
+        gb, outs = resident
+
+    def shade_into(o):
+        ctx.shade_frame(gb, o, fmt=N.PBR_OUTPUT_RGBA8_UNORM, stream=stream)
+
+    wall, ms = shade_steps(shade_into, outs, stream, max(args.warmup, 3), args.steps)
+    px = cfg5.width * rows
+    return {"workload": f"{cfg5.name}_band{rows}", "output": "rgba8", "mode": args.mode, "px_per_step": px,
+            "value": round(px * args.steps / wall / 1e6, 2), "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "shade_ms": round(float(np.mean(ms)), 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -254,6 +370,8 @@ def main():
                          "profiles/r01 kernel trace); not a step, no gather")
     ap.add_argument("--config", type=int, default=0, help="BASELINE config id (default 3 at N=1, 5 at N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-anchor", action="store_true",
+                    help="skip the scaling anchor (one rank's config-5 band shaded alone, scale_anchor)")
     ap.add_argument("--rows-per-rank", type=int, default=1024,
                     help="config 5 band height per rank (1024 = the BASELINE geometry: 8192x8192 at N = 8; "
                          "smaller only for rehearsing the multi-rank path). The same band at every N, N = 1 "
@@ -308,26 +426,12 @@ def main():
     band = D.band_rows(cfg.height, world, rank)
     workload = f"{cfg.name}" + (f"_band{args.rows_per_rank}" if banded else "")
 
-    t0 = time.perf_counter()
-    pc = S.scene_pass(cfg)
-    if args.mode == "faithful":
-        pc.flags = int(pc.flags) | N.PBR_FLAG_FAITHFUL
-    env = S.env_map() if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
-    staging = torch.empty((N.NUM_PLANES, band.rows, cfg.width), dtype=torch.float32, pin_memory=True)
-    S.fill_gbuffer_host(cfg, band.row_begin, band.row_end, out=staging.numpy())
-    t_fill = time.perf_counter() - t0
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    planes_dev = staging.to(device, non_blocking=True)
-    torch.cuda.synchronize()
-    t_upload = time.perf_counter() - t1
-    from physically_based_renderer_amd.renderer import GBuffer
-
-    gb = GBuffer(planes_dev)
+    pc, env, staging, gb, t_fill, t_upload = make_workload(cfg, band, args.mode, device)
     ctx = ShadingContext(device.index)
-    ctx.set_pass(pc)
+    stream = torch.cuda.current_stream(device)
+    ctx.set_pass(pc, stream)
     if env is not None:
-        ctx.set_env_map(env)
+        ctx.set_env_map(env, stream)
     log(f"rank {rank}/{world}: {workload} rows [{band.row_begin},{band.row_end}) fill {t_fill:.2f}s "
         f"upload {t_upload * 1e3:.1f} ms ({staging.numel() * 4 / t_upload / 1e9:.1f} GB/s H2D)"
         + (f", process group {dist.get_backend()}" if in_group else ""))
@@ -338,25 +442,12 @@ def main():
     fmt = N.PBR_OUTPUT_RGBA8_UNORM if rgba8 else N.PBR_OUTPUT_RGBA32F
     outs = [torch.empty((band.rows_max, cfg.width, 4), dtype=out_dtype, device=device) for _ in range(2)]
     gather = D.BandGather(band, cfg.width, device, dtype=out_dtype) if banded else None
-    stream = torch.cuda.current_stream(device)
-    pending = [[], []]
 
     def shade_into(o):
         if rgba8:
             ctx.shade_frame(gb, o, fmt=fmt, stream=stream)
         else:
             ctx.shade(gb, o, stream)
-
-    def step(k: int, ev=None):
-        slot = k % 2
-        D.BandGather.wait(pending[slot])  # the gather that last read this slot (stream-side wait)
-        if ev is not None:
-            ev[0].record(stream)
-        shade_into(outs[slot])
-        if ev is not None:
-            ev[1].record(stream)
-        if gather is not None:
-            pending[slot] = gather.start(outs[slot])
 
     # GPU clock ramp (see --ramp-ms): full shading passes, untimed, before the W warm-up steps.
     t_ramp = time.perf_counter()
@@ -369,33 +460,14 @@ def main():
             if time.perf_counter() - t_ramp >= args.ramp_ms / 1e3:
                 break
     ramp_ms = (time.perf_counter() - t_ramp) * 1e3
-    for k in range(args.warmup):
-        step(k)
-    for p in pending:
-        D.BandGather.wait(p)
-    pending = [[], []]
-    torch.cuda.synchronize()
-    if in_group:
-        dist.barrier()
-    torch.cuda.synchronize()
+    elapsed, kernel_ms = shade_steps(shade_into, outs, stream, args.warmup, args.steps, gather, in_group)
 
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t_start = time.perf_counter()
-    for k in range(args.steps):
-        step(k, events[k])
-    for p in pending:
-        D.BandGather.wait(p)
-    torch.cuda.synchronize()
-    if in_group:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    kernel_ms = [a.elapsed_time(b) for a, b in events]
-
+    # The executed work of the last timed pass (pbr_last_pass_stats; every timed pass shades the same input).
+    stats = ctx.pass_stats(stream)
     cull_note = {}
     if pc.flags & N.PBR_FLAG_TILED_CULLING:
-        kept, tiles = ctx.cull_stats(stream)  # of the last timed pass
-        cull_note = {"lights_per_tile": round(kept / max(tiles, 1), 3), "tiles": tiles}
+        cull_note = {"lights_per_tile": round(stats["cull_tile_lights"] / max(stats["cull_tiles"], 1), 3),
+                     "tiles": stats["cull_tiles"]}
 
     coll_dev = device if args.dist_backend == "nccl" else torch.device("cpu")
     gather_note = {}
@@ -446,19 +518,21 @@ def main():
         band_px = cfg.width * band.rows
         bpp = bytes_per_pixel(pc, 4 if rgba8 else 16)
         achieved = bpp * band_px / avg_kernel_s / 1e9
-        traffic, valu_busy = load_pmc(workload + ("_rgba8" if rgba8 and not banded else "")
-                                      + ("_faithful" if args.mode == "faithful" else ""))
+        traffic, valu_busy, pmc_prov = load_pmc(workload + ("_rgba8" if rgba8 and not banded else "")
+                                                + ("_faithful" if args.mode == "faithful" else ""))
         tile_px = 256 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 128  # culling unit: 32x8 / 64x2
         fpp = flops_per_pixel(pc, cull_note.get("lights_per_tile"), tile_px)
+        fpp_exec = executed_flops_per_pixel(pc, stats, band_px)
         tflops = fpp * band_px / avg_kernel_s / 1e12
+        tflops_exec = fpp_exec * band_px / avg_kernel_s / 1e12
         # At 64 lights the arithmetic intensity (fpp / bpp ~ 99 FLOP/B) is 5x the ridge point, so the
         # FP32 vector (VALU) roof bounds the kernel: 157.3 TF (MI355X_MICROARCH.md). There is no matrix op
-        # on this path. HBM is reported beside it.
+        # on this path; "mfma" is the contract's name for the compute roof. HBM is reported beside it.
         compute_bound = fpp / bpp > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
         hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                "frac": round(achieved / HBM_PEAK_GBPS, 5)}
         roofline = {
-            "bound": "valu" if compute_bound else "hbm",
+            "bound": "mfma" if compute_bound else "hbm",
             "achieved": round(tflops, 3) if compute_bound else hbm["achieved"],
             "peak": FP32_PEAK_TFLOPS if compute_bound else HBM_PEAK_GBPS,
             "unit": "TFLOP/s" if compute_bound else "GB/s",
@@ -467,12 +541,22 @@ def main():
             "kernel": "shade_tile_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 4),
             "median_launch_ms": round(median_kernel_ms, 4),
             "flop_per_px": fpp, "bytes_per_px": bpp, "px_per_launch": band_px,
+            "executed_flop_per_px": fpp_exec,
+            "achieved_executed": round(tflops_exec, 3),
+            "frac_executed": round(tflops_exec / FP32_PEAK_TFLOPS, 4),
+            "pass_stats": {k: stats[k] for k in ("geometry_pixels", "light_terms", "backface_tests",
+                                                 "cull_tiles", "exact_pixels")},
             "hbm": hbm,
             "valu_issue_busy": valu_busy,
-            "note": ("compute roof = the FP32 vector ALU (VALU, 157.3 TF packed; no matrix op on this path); "
-                     "achieved counts the HLSL-level FLOPs (SURVEY 8(d)); traffic = rocprofv3 FETCH_SIZE + "
-                     "WRITE_SIZE bytes per launch and valu_issue_busy = SQ_ACTIVE_INST_VALU over kernel cycles, "
-                     "both from profiles/pmc_summary.json"),
+            "pmc": pmc_prov,
+            "note": ("compute roof = the FP32 vector ALU (VALU, 157.3 TF packed; no matrix op on this path; 'mfma' is "
+                     "the contract's name for the compute roof); achieved / frac count SURVEY 8(d)'s algorithmic "
+                     "FLOPs (every light for every pixel); achieved_executed / frac_executed count only the terms "
+                     "the kernel evaluated (pass_stats: back-facing terms skipped by the wave-balanced lists and "
+                     "culled lights are not credited; the lists' back-face tests are); traffic = rocprofv3 "
+                     "FETCH_SIZE x2 + WRITE_SIZE bytes per launch and valu_issue_busy = SQ_ACTIVE_INST_VALU over "
+                     "kernel cycles, from profiles/pmc_summary.json, quoted only when its kernel_sources_sha "
+                     "equals this build's (pmc)"),
         }
         cpu = None
         parity = {}
@@ -490,6 +574,14 @@ def main():
         elif world > 1 and gather is not None and args.parity_rows > 0:
             parity = {"gathered_frame_parity": gathered_parity(cfg, pc, env, gather.assembled(cfg.height).cpu().numpy(),
                                                                world, args.parity_rows, rgba8)}
+        scale = {}
+        if not args.no_anchor:
+            anchor = band_anchor(ctx, args, world, device, stream, (gb, outs) if banded and rgba8 else None)
+            scale = {"scale_anchor": anchor}
+            if world > 1:
+                per_rank = value / world
+                scale.update({"per_rank_mpix_s": round(per_rank, 2),
+                              "efficiency_vs_anchor": round(per_rank / anchor["value"], 4)})
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpix/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "clock_ramp": {"ms": round(ramp_ms, 1), "launches": n_ramp},
@@ -505,7 +597,7 @@ def main():
             "hbm_gbps": round(achieved, 2),
             "roofline": roofline,
             "cpu_baseline": cpu,
-            **parity, **gather_note, **cull_note,
+            **parity, **gather_note, **cull_note, **scale,
             **({"exact_mode": exact_leg} if exact_leg is not None else {}),
             "pcie_h2d_gbps": round(staging.numel() * 4 / t_upload / 1e9, 2),
         }

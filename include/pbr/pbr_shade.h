@@ -12,8 +12,13 @@
  *   - every function returns int: 0 = PBR_OK, negative = pbr_status; no exception crosses the ABI;
  *   - the caller owns every buffer passed in; the library never frees them;
  *   - device work is stream-ordered and asynchronous on the hipStream_t given (NULL = default
- *     stream); a context is bound to one device and may be used from several streams, but calls
- *     that change its state (pbr_set_pass, pbr_set_env_map) are ordered only on their own stream.
+ *     stream); a context is bound to one device and is reentrant across streams, like the
+ *     reference's 3-deep frame-resource ring (FrameResource.h:111-140, PBRApp.cpp:220-243): every
+ *     pbr_set_pass uploads into its own device light slot, a pass reads the slot of the
+ *     pbr_set_pass before it and waits (stream-side) for that upload when it was made on another
+ *     stream, and a slot or texture is overwritten only after the queued passes that read it, on
+ *     whatever stream they run. Host calls on one context are serialised by its mutex; the host
+ *     order of pbr_set_pass and pbr_shade_* calls decides which pass a shade uses.
  * Plain C types only (hipStream_t is passed as void*).
  */
 #ifndef PBR_SHADE_H
@@ -25,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PBR_ABI_VERSION 4
+#define PBR_ABI_VERSION 5
 #define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
 
 typedef enum pbr_status {
@@ -170,8 +175,8 @@ int pbr_set_sky_map_f32(pbr_context* ctx, const float* texels, int32_t width, in
  * format conversion are fused into the shading kernel). Asynchronous on `stream`. */
 int pbr_shade_frame(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* frame, void* stream);
 
-/* Tiled-culling statistics of the last pass on `stream` (synchronises that stream), zeros when that
- * pass did not cull:
+/* Tiled-culling statistics of the last pass on `stream` (synchronises that stream; see
+ * pbr_last_pass_stats for which pass), zeros when that pass did not cull:
  * total surviving point/spot lights summed over the culling tiles that hold geometry, and the number
  * of those tiles. A culling tile is one wave64's pixels (64x2 in the default pixel-pair layout, 32x8
  * workgroups in the one-pixel layout). The kernel writes per-workgroup counts (no atomics); this
@@ -187,11 +192,22 @@ typedef struct pbr_pass_stats {
     int64_t exact_pixels;     /* geometry pixels whose light sum the exact path re-evaluated (inputs or
                                  intermediates outside the fast-path window; every geometry pixel with
                                  PBR_FLAG_EXACT_ONLY) */
+    /* ABI 5: the work the light loops executed (what a FLOP count of the pass may credit). */
+    int64_t light_terms;      /* (geometry pixel, light) terms evaluated: every light of the pass in the
+                                 uniform loop, the survivors of the culling tile under PBR_FLAG_TILED_CULLING,
+                                 the live (front-facing, in the wave-balanced lists) point lights plus the
+                                 directional ones in a wave-balanced pass. The exact re-pass of
+                                 exact_pixels is not counted. */
+    int64_t geometry_pixels;  /* pixels shaded by PS (the coverage plane's non-zero pixels; all without one) */
+    int64_t backface_tests;   /* wave-balanced passes: (pixel, point light) back-face tests of the list
+                                 build (4 FMAs each); 0 otherwise */
 } pbr_pass_stats;
 
-/* Fill *out with the statistics of the last pbr_shade_gbuffer / pbr_shade_frame call (synchronises
- * `stream`, which must be the stream that pass ran on or one ordered after it). All zero before the
- * first pass. The kernel writes one record per workgroup; this call sums them on the host. */
+/* Fill *out with the statistics of the last pbr_shade_gbuffer / pbr_shade_frame call on `stream`
+ * (synchronises `stream`). Each stream keeps its own record, so passes on other streams never mix
+ * into it; if the context has not shaded on `stream`, the context's last pass on any stream is
+ * reported, and `stream` must then be ordered after that pass. All zero before the first pass.
+ * The kernel writes one record per wave (workgroup in the one-pixel layout); this call sums them. */
 int pbr_last_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream);
 
 /* ---- Host G-buffer fill (replaces the VS + rasteriser front-end, Default.hlsl:22-45) ---------- */

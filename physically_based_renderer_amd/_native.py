@@ -131,6 +131,9 @@ class PassStats(ctypes.Structure):
         ("cull_tiles", ctypes.c_int64),
         ("cull_tile_lights", ctypes.c_int64),
         ("exact_pixels", ctypes.c_int64),
+        ("light_terms", ctypes.c_int64),
+        ("geometry_pixels", ctypes.c_int64),
+        ("backface_tests", ctypes.c_int64),
     ]
 
 
@@ -202,6 +205,21 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         _lib = handle
     return _lib
+
+
+def kernel_sources_sha(csrc_dir: str = CSRC_DIR) -> str:
+    """sha256 (first 16 hex digits) of the sources libpbrshade.so is built from (csrc/*.hip, *.h, *.cpp, the
+    Makefile) and the public header: the revision stamp of committed profiles (profiles/pmc_summary.json), so
+    that bench.py quotes counters only when they were measured on the kernels it runs."""
+    import hashlib
+
+    h = hashlib.sha256()
+    names = sorted(n for n in os.listdir(csrc_dir) if n.endswith((".hip", ".h", ".cpp")) or n == "Makefile")
+    for path in [os.path.join(csrc_dir, n) for n in names] + [HEADER_PATH]:
+        h.update(os.path.basename(path).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def status_string(status: int) -> str:

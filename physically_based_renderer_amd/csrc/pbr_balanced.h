@@ -453,6 +453,15 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
     return BalMasks{a0, a1, c0, c1};
 }
 
+// The wave's live (pixel, light) items -- the popcounts of its pixels' live masks, summed over the wave: the
+// point-light terms pass 2 evaluates (statistics: pbr_pass_stats::light_terms). Wave-uniform result.
+__device__ __forceinline__ int wave_live_items(const BalMasks& bm) {
+    int c = (__popc(bm.a0) + __popc(bm.a1)) + (__popc(bm.c0) + __popc(bm.c1));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+    return __builtin_amdgcn_readfirstlane(c);
+}
+
 // The whole balanced pass over the point lights of an untiled lean wave (at most kBalMaxLights). `live_a` /
 // `live_b` say which of the pair's pixels take part (geometry); `lds_lights`: the pass's point lights staged by
 // the block (stage_balanced_lights); `bm`: their live masks from balanced_pass1. ORs the pixels that left the

@@ -14,17 +14,55 @@
 #include "pbr/pbr_shade.h"
 #include "shade_kernels.h"
 
+// Cross-stream ordering of the context's device resources (the reference's 3-deep FrameResource ring,
+// FrameResource.h:111-140, PBRApp.cpp:220-243, is the same idea on D3D12 fences). A resource -- a light slot,
+// the env map, the sky map -- remembers which streams have queued a pass reading it since it was last written
+// and which stream wrote it (with an event after the write):
+//   * before it is overwritten on stream w, w waits (stream-side, no host synchronisation) for the last pass of
+//     every other stream that read it -- each stream's `last_pass` event, recorded after its launches;
+//     waiting for a later pass of that stream is merely early;
+//   * a pass on stream s that reads it waits for the write's event once, unless s wrote it.
+// A context used from one stream records nothing per launch (every reader is the writer's stream). The first
+// launch on a second stream synchronises the device once, so the earlier single-stream passes are complete and
+// need no event; from then on each launch records its stream's last_pass.
+struct StreamState {
+    hipStream_t stream = nullptr;
+    hipEvent_t last_pass = nullptr;  // multi-stream contexts: recorded after every launch on `stream`
+    // Statistics of the last pass on this stream: one record of pbr::kStatsPerBlock int32 per statistics slot
+    // (one per wave in the pair layout, per workgroup in the one-pixel layout; pbr::StatField), summed on the
+    // host by pbr_last_pass_stats / pbr_last_cull_stats. Written only by this stream's passes, so a pass never
+    // overwrites the record of a pass on another stream.
+    int32_t* d_stats = nullptr;
+    int64_t stats_capacity = 0;  // slots
+    int64_t tiles = 0, slots = 0;
+    bool culled = false;
+};
+
+struct Resource {
+    std::vector<int> readers;  // StreamState indices that launched a pass reading it since the last write
+    int writer = -1;           // StreamState index of the stream that wrote it last (-1: none / host-complete)
+    hipEvent_t written = nullptr;  // recorded on the writer's stream after the write
+};
+
 struct pbr_context {
     int device = 0;
-    // Lights: device copy (3 float4 per light) fed from a small pinned ring so a host pass struct can
-    // be reused as soon as pbr_set_pass returns while the copy is still in flight.
-    float4* d_lights = nullptr;
-    int lights_capacity = 0;
-    static constexpr int kRing = 4;
-    pbr_light* h_ring[kRing] = {};
-    hipEvent_t ring_done[kRing] = {};
-    bool ring_used[kRing] = {};
-    int ring_next = 0;
+    std::vector<StreamState> streams;
+    // Lights: a ring of device slots (3 float4 per light), each fed from its own pinned staging copy so a host
+    // pass struct can be reused as soon as pbr_set_pass returns. Every pbr_set_pass takes the next slot; a
+    // launch reads the slot of the pass it was queued with, so setting frame k+1's pass (on any stream) never
+    // overwrites the lights a queued frame k reads.
+    static constexpr int kSlots = 4;
+    struct LightSlot {
+        float4* d = nullptr;
+        int capacity = 0;
+        pbr_light* h = nullptr;        // pinned staging, PBR_MAX_LIGHTS records
+        hipEvent_t copied = nullptr;   // the staging -> device copy
+        bool copy_pending = false;
+        Resource use;
+    };
+    LightSlot slots[kSlots];
+    int cur_slot = -1;
+    int next_slot = 0;
     // Textures: the environment (IBL, g_SkyArray[1]) and the sky (g_SkyArray[0]), each kept as fp32
     // RGBA on the device (decoded once from R16G16B16A16_UNORM, or uploaded as fp32).
     struct Texture {
@@ -32,6 +70,7 @@ struct pbr_context {
         float4* d = nullptr;
         int w = 0, h = 0, capacity = 0;
         bool nonneg = true;  // no negative or NaN texel (PBR_FLAG_FAITHFUL precondition for the IBL)
+        Resource use;
     };
     Texture env, sky;
     // Current pass.
@@ -41,15 +80,7 @@ struct pbr_context {
     bool pass_set = false;
     bool faithful_pass_ok = false;  // light strengths and the constant ambient are finite and >= 0
     bool faithful_count_terms = false;  // > 64 lights (culled pass): the kernel counts summed terms per wave
-    // Statistics of the last pass: one record of pbr::kStatsPerBlock int32 per statistics slot (one per wave
-    // in the pair layout, per workgroup in the one-pixel layout; [surviving
-    // point/spot lights summed over its culling tiles, culling tiles with geometry, pixels redone by the
-    // exact path]), summed on the host by pbr_last_pass_stats / pbr_last_cull_stats.
-    int32_t* d_tile_kept = nullptr;
-    int64_t tile_kept_capacity = 0;
-    int64_t last_tiles = 0;
-    int64_t last_slots = 0;  // statistics records of the last pass (shade_stat_slots_per_tile per tile)
-    bool last_culled = false;
+    int last_stream = -1;  // StreamState index of the context's last pass (pbr_last_pass_stats fallback)
     // Wave-balanced point-light lists (pbr_balanced.h) for untiled passes with at least this many point lights
     // and no spot lights; -1: the measured crossover of the mode (kBalancedMinFaithful / kBalancedMinExact);
     // PBR_BALANCED_MIN overrides both (0 disables).
@@ -82,6 +113,87 @@ int fail_hip(pbr_context* ctx, hipError_t e, const char* what, int status = PBR_
 }
 
 bool is_ambient_mode(int m) { return m == PBR_AMBIENT_CONSTANT || m == PBR_AMBIENT_IBL_DIFFUSE; }
+
+void forget_readers(pbr_context* ctx);
+
+// The StreamState of `s` (created on first use). Caller holds ctx->mu and the device guard. A new stream
+// beside existing ones: the device is synchronised once, so every pass queued so far is complete and no
+// resource has a pending reader (the single-stream passes recorded no event).
+int stream_index(pbr_context* ctx, hipStream_t s, hipError_t& e) {
+    for (size_t i = 0; i < ctx->streams.size(); ++i)
+        if (ctx->streams[i].stream == s) return (int)i;
+    if (!ctx->streams.empty()) {
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) return -1;
+        forget_readers(ctx);
+    }
+    StreamState st;
+    st.stream = s;
+    // device-scope release: only other streams of this device (and host waits before a free) observe it
+    e = hipEventCreateWithFlags(&st.last_pass, hipEventDisableTiming | hipEventReleaseToDevice);
+    if (e != hipSuccess) return -1;
+    ctx->streams.push_back(st);
+    return (int)ctx->streams.size() - 1;
+}
+
+// Order a write of `r` on stream `w` (index wi) after every pass of another stream that read it.
+hipError_t before_write(pbr_context* ctx, Resource& r, hipStream_t w, int wi) {
+    for (int i : r.readers) {
+        if (i == wi) continue;  // same stream: already ordered
+        const hipError_t e = hipStreamWaitEvent(w, ctx->streams[i].last_pass, 0);
+        if (e != hipSuccess) return e;
+    }
+    r.readers.clear();
+    return hipSuccess;
+}
+
+// Wait on the host for every reader of `r` (before freeing its memory).
+hipError_t before_free(pbr_context* ctx, Resource& r) {
+    for (int i : r.readers) {
+        const hipError_t e = hipEventSynchronize(ctx->streams[i].last_pass);
+        if (e != hipSuccess) return e;
+    }
+    r.readers.clear();
+    if (r.writer >= 0 && r.written) {
+        const hipError_t e = hipEventSynchronize(r.written);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// Record the write of `r` on stream `w` (index wi).
+hipError_t after_write(Resource& r, hipStream_t w, int wi) {
+    if (!r.written) {
+        const hipError_t e = hipEventCreateWithFlags(&r.written, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    r.writer = wi;
+    return hipEventRecord(r.written, w);
+}
+
+// A pass on stream `s` (index si) is about to read `r`: order it after the write, once per stream.
+hipError_t before_read(Resource& r, hipStream_t s, int si) {
+    for (int i : r.readers)
+        if (i == si) return hipSuccess;
+    if (r.writer >= 0 && r.writer != si) {
+        const hipError_t e = hipStreamWaitEvent(s, r.written, 0);
+        if (e != hipSuccess) return e;
+    }
+    r.readers.push_back(si);
+    return hipSuccess;
+}
+
+// After a device synchronisation: every queued read and write of the context's resources is complete.
+void forget_readers(pbr_context* ctx) {
+    for (pbr_context::LightSlot& sl : ctx->slots) {
+        sl.use.readers.clear();
+        sl.use.writer = -1;
+    }
+    for (pbr_context::Texture* t : {&ctx->env, &ctx->sky}) {
+        t->use.readers.clear();
+        t->use.writer = -1;
+    }
+}
 
 }  // namespace
 
@@ -122,10 +234,10 @@ int pbr_context_create(int device, pbr_context** out_ctx) {
         return PBR_ERR_NO_DEVICE;
     }
     hipError_t e = hipSuccess;
-    for (int i = 0; e == hipSuccess && i < pbr_context::kRing; ++i) {
-        e = hipHostMalloc(reinterpret_cast<void**>(&ctx->h_ring[i]), sizeof(pbr_light) * PBR_MAX_LIGHTS,
+    for (int i = 0; e == hipSuccess && i < pbr_context::kSlots; ++i) {
+        e = hipHostMalloc(reinterpret_cast<void**>(&ctx->slots[i].h), sizeof(pbr_light) * PBR_MAX_LIGHTS,
                           hipHostMallocDefault);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ring_done[i], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->slots[i].copied, hipEventDisableTiming);
     }
     if (e != hipSuccess) {
         pbr_context_destroy(ctx);
@@ -140,16 +252,21 @@ int pbr_context_destroy(pbr_context* ctx) {
     {
         DeviceGuard g(ctx->device);
         (void)hipDeviceSynchronize();
-        for (int i = 0; i < pbr_context::kRing; ++i) {
-            if (ctx->ring_done[i]) (void)hipEventDestroy(ctx->ring_done[i]);
-            if (ctx->h_ring[i]) (void)hipHostFree(ctx->h_ring[i]);
+        for (pbr_context::LightSlot& sl : ctx->slots) {
+            if (sl.copied) (void)hipEventDestroy(sl.copied);
+            if (sl.h) (void)hipHostFree(sl.h);
+            if (sl.d) (void)hipFree(sl.d);
+            if (sl.use.written) (void)hipEventDestroy(sl.use.written);
         }
-        if (ctx->d_lights) (void)hipFree(ctx->d_lights);
         for (pbr_context::Texture* t : {&ctx->env, &ctx->sky}) {
             if (t->d_u16) (void)hipFree(t->d_u16);
             if (t->d) (void)hipFree(t->d);
+            if (t->use.written) (void)hipEventDestroy(t->use.written);
         }
-        if (ctx->d_tile_kept) (void)hipFree(ctx->d_tile_kept);
+        for (StreamState& st : ctx->streams) {
+            if (st.last_pass) (void)hipEventDestroy(st.last_pass);
+            if (st.d_stats) (void)hipFree(st.d_stats);
+        }
     }
     delete ctx;
     return PBR_OK;
@@ -171,37 +288,42 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipError_t e;
-    if (n > ctx->lights_capacity) {
-        // Growing: the old buffer may still be read by queued kernels on any stream.
-        if (ctx->d_lights) {
-            e = hipDeviceSynchronize();
-            if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass sync");
-            (void)hipFree(ctx->d_lights);
-            ctx->d_lights = nullptr;
-            ctx->lights_capacity = 0;
+    hipError_t e = hipSuccess;
+    const int si = stream_index(ctx, s, e);
+    if (si < 0) return fail_hip(ctx, e, "pbr_set_pass stream");
+    // The next slot of the ring: its staging copy must have left the host buffer, and its device copy is
+    // overwritten only after the queued passes that read it (stream-side waits, before_write).
+    const int slot = ctx->next_slot;
+    pbr_context::LightSlot& sl = ctx->slots[slot];
+    if (sl.copy_pending) {
+        e = hipEventSynchronize(sl.copied);
+        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass staging wait");
+        sl.copy_pending = false;
+    }
+    if (n > sl.capacity) {
+        // Growing: the old buffer may still be read by queued passes.
+        if (sl.d) {
+            e = before_free(ctx, sl.use);
+            if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass slot wait");
+            (void)hipFree(sl.d);
+            sl.d = nullptr;
+            sl.capacity = 0;
         }
         int cap = 64;
         while (cap < n) cap *= 2;
-        e = hipMalloc(&ctx->d_lights, sizeof(pbr_light) * (size_t)cap);
+        e = hipMalloc(&sl.d, sizeof(pbr_light) * (size_t)cap);
         if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass hipMalloc");
-        ctx->lights_capacity = cap;
+        sl.capacity = cap;
     }
     bool points_ok = true;  // every point light's fast-path flag is set (the balanced pass needs it)
     if (n > 0) {
-        const int slot = ctx->ring_next;
-        ctx->ring_next = (slot + 1) % pbr_context::kRing;
-        if (ctx->ring_used[slot]) {
-            e = hipEventSynchronize(ctx->ring_done[slot]);
-            if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass ring wait");
-        }
-        std::memcpy(ctx->h_ring[slot], pass->lights, sizeof(pbr_light) * (size_t)n);
+        std::memcpy(sl.h, pass->lights, sizeof(pbr_light) * (size_t)n);
         // The kernel's per-light fast-path flag travels in the unused pad1 of the uploaded copy
         // (the caller's array is not touched): directional L = -Direction components, point / spot
         // positions, each 0 or |x| in [2^-20, 16] / [2^-20, 2^20] (pbr_device_math.h, light_window_ok),
         // and a finite point / spot strength.
         for (long long i = 0; i < n; ++i) {
-            pbr_light& L = ctx->h_ring[slot][i];
+            pbr_light& L = sl.h[i];
             const bool directional = i < nd;
             const float* c = directional ? L.direction : L.position;
             const float hi = directional ? 16.0f : 0x1p20f;
@@ -216,12 +338,18 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
             L.pad1 = ok ? 1.0f : 0.0f;
             if (i >= nd && i < nd + np) points_ok = points_ok && ok;
         }
-        e = hipMemcpyAsync(ctx->d_lights, ctx->h_ring[slot], sizeof(pbr_light) * (size_t)n, hipMemcpyHostToDevice, s);
+        e = before_write(ctx, sl.use, s, si);
+        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass order");
+        e = hipMemcpyAsync(sl.d, sl.h, sizeof(pbr_light) * (size_t)n, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass copy");
-        e = hipEventRecord(ctx->ring_done[slot], s);
+        e = hipEventRecord(sl.copied, s);
         if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass record");
-        ctx->ring_used[slot] = true;
+        sl.copy_pending = true;
+        e = after_write(sl.use, s, si);
+        if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass record");
     }
+    ctx->cur_slot = slot;
+    ctx->next_slot = (slot + 1) % pbr_context::kSlots;
     pbr::PassArgs& p = ctx->pass;
     for (int i = 0; i < 3; ++i) {
         p.eye[i] = pass->eye_pos_w[i];
@@ -270,10 +398,12 @@ int set_texture(pbr_context* ctx, pbr_context::Texture& t, const void* texels, b
     if (!g.ok) return PBR_ERR_NO_DEVICE;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int n = width * height;
-    hipError_t e;
+    hipError_t e = hipSuccess;
+    const int si = stream_index(ctx, s, e);
+    if (si < 0) return fail_hip(ctx, e, what);
     if (n > t.capacity) {
-        // Growing: the old texture may still be read by queued kernels on any stream.
-        e = hipDeviceSynchronize();
+        // Growing: the old texture may still be read by queued passes.
+        e = before_free(ctx, t.use);
         if (e != hipSuccess) return fail_hip(ctx, e, what);
         if (t.d_u16) (void)hipFree(t.d_u16);
         if (t.d) (void)hipFree(t.d);
@@ -285,6 +415,9 @@ int set_texture(pbr_context* ctx, pbr_context::Texture& t, const void* texels, b
         if (e != hipSuccess) return fail_hip(ctx, e, what);
         t.capacity = n;
     }
+    // Replaced in place: after the queued passes (of any stream) that read the old texels.
+    e = before_write(ctx, t.use, s, si);
+    if (e != hipSuccess) return fail_hip(ctx, e, what);
     if (unorm16) {
         e = hipMemcpyAsync(t.d_u16, texels, sizeof(uint16_t) * 4 * (size_t)n, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return fail_hip(ctx, e, what);
@@ -296,6 +429,7 @@ int set_texture(pbr_context* ctx, pbr_context::Texture& t, const void* texels, b
     }
     e = hipStreamSynchronize(s);  // the (pageable) host texels may be released on return
     if (e != hipSuccess) return fail_hip(ctx, e, what);
+    t.use.writer = -1;  // complete: later passes on any stream see the new texels
     t.w = width;
     t.h = height;
     t.nonneg = true;
@@ -349,7 +483,7 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     a.ps.env_h = ctx->env.h;
     a.ps.sky_w = ctx->sky.w;
     a.ps.sky_h = ctx->sky.h;
-    a.lights = ctx->d_lights;
+    a.lights = ctx->cur_slot >= 0 ? ctx->slots[ctx->cur_slot].d : nullptr;
     a.env = ctx->env.d;
     a.frame.out = fr->out;
     a.frame.out_stride = fr->out_row_stride;
@@ -385,30 +519,44 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipError_t e;
+    hipError_t e = hipSuccess;
+    const int si = stream_index(ctx, s, e);
+    if (si < 0) return fail_hip(ctx, e, "shade stream");
+    StreamState& st = ctx->streams[si];
     {
         const int64_t tiles = pbr::shade_tile_count(gb->width, gb->height, a.pixels_per_thread);
         const int64_t slots = tiles * pbr::shade_stat_slots_per_tile(a.pixels_per_thread);
-        if (slots > ctx->tile_kept_capacity) {
-            // Growing: the old buffer may still be written by queued kernels on any stream.
-            if (ctx->d_tile_kept) {
-                e = hipDeviceSynchronize();
+        if (slots > st.stats_capacity) {
+            // Growing: only this stream's passes write the buffer (stream order covers them).
+            if (st.d_stats) {
+                e = hipStreamSynchronize(s);
                 if (e != hipSuccess) return fail_hip(ctx, e, "pass stats sync");
-                (void)hipFree(ctx->d_tile_kept);
-                ctx->d_tile_kept = nullptr;
-                ctx->tile_kept_capacity = 0;
+                (void)hipFree(st.d_stats);
+                st.d_stats = nullptr;
+                st.stats_capacity = 0;
             }
-            e = hipMalloc(&ctx->d_tile_kept, pbr::kStatsPerBlock * sizeof(int32_t) * (size_t)slots);
+            e = hipMalloc(&st.d_stats, pbr::kStatsPerBlock * sizeof(int32_t) * (size_t)slots);
             if (e != hipSuccess) return fail_hip(ctx, e, "pass stats hipMalloc");
-            ctx->tile_kept_capacity = slots;
+            st.stats_capacity = slots;
         }
-        ctx->last_tiles = tiles;
-        ctx->last_slots = slots;
-        ctx->last_culled = cull;
-        a.tile_kept = ctx->d_tile_kept;
+        st.tiles = tiles;
+        st.slots = slots;
+        st.culled = cull;
+        a.tile_kept = st.d_stats;
     }
+    // Order the pass after the writes of what it reads (lights, textures) made on other streams.
+    const bool reads_lights = ctx->cur_slot >= 0 && a.ps.n_dir + a.ps.n_point + a.ps.n_spot > 0;
+    if (reads_lights) e = before_read(ctx->slots[ctx->cur_slot].use, s, si);
+    if (e == hipSuccess && ctx->ambient_mode == PBR_AMBIENT_IBL_DIFFUSE) e = before_read(ctx->env.use, s, si);
+    if (e == hipSuccess && fr->coverage) e = before_read(ctx->sky.use, s, si);
+    if (e != hipSuccess) return fail_hip(ctx, e, "shade order");
     e = pbr::launch_shade(a, s);
     if (e != hipSuccess) return fail_hip(ctx, e, "shade_tile_kernel launch", PBR_ERR_LAUNCH);
+    if (ctx->streams.size() > 1) {
+        e = hipEventRecord(st.last_pass, s);
+        if (e != hipSuccess) return fail_hip(ctx, e, "shade record");
+    }
+    ctx->last_stream = si;
     return PBR_OK;
 }
 
@@ -453,24 +601,33 @@ int pbr_shade_frame(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame
 
 namespace {
 
-// Sum the per-workgroup records of the last pass.
+// Sum the statistics records of the last pass on `stream` (or, if the context never launched on that stream,
+// of its last pass on any stream: the caller's stream is then ordered after it by contract).
 int sum_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream, const char* what) {
     *out = pbr_pass_stats{};
     DeviceGuard g(ctx->device);
     if (!g.ok) return PBR_ERR_NO_DEVICE;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (ctx->last_tiles == 0) return PBR_OK;  // no pass yet (or an empty frame)
-    std::vector<int32_t> h(pbr::kStatsPerBlock * (size_t)ctx->last_slots);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipError_t e = hipMemcpyAsync(h.data(), ctx->d_tile_kept, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s);
+    int si = -1;
+    for (size_t i = 0; i < ctx->streams.size(); ++i)
+        if (ctx->streams[i].stream == s && ctx->streams[i].tiles > 0) si = (int)i;
+    if (si < 0) si = ctx->last_stream;
+    if (si < 0 || ctx->streams[si].tiles == 0) return PBR_OK;  // no pass yet (or an empty frame)
+    const StreamState& st = ctx->streams[si];
+    std::vector<int32_t> h(pbr::kStatsPerBlock * (size_t)st.slots);
+    hipError_t e = hipMemcpyAsync(h.data(), st.d_stats, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail_hip(ctx, e, what);
-    out->workgroups = ctx->last_tiles;
-    out->culled = ctx->last_culled ? 1 : 0;
+    out->workgroups = st.tiles;
+    out->culled = st.culled ? 1 : 0;
     for (size_t t = 0; t < h.size(); t += pbr::kStatsPerBlock) {
-        out->cull_tile_lights += h[t];
-        out->cull_tiles += h[t + 1];
-        out->exact_pixels += h[t + 2];
+        out->cull_tile_lights += h[t + pbr::kStatCullKept];
+        out->cull_tiles += h[t + pbr::kStatCullTiles];
+        out->exact_pixels += h[t + pbr::kStatExactPixels];
+        out->light_terms += h[t + pbr::kStatLightTerms];
+        out->geometry_pixels += h[t + pbr::kStatGeometryPixels];
+        out->backface_tests += h[t + pbr::kStatBackfaceTests];
     }
     return PBR_OK;
 }

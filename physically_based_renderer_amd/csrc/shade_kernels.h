@@ -47,7 +47,16 @@ struct FrameArgs {
     const float4* sky;         // sky_w * sky_h RGBA fp32 (required when coverage != nullptr)
 };
 
-constexpr int kStatsPerBlock = 3;
+// One statistics record (int32 each): its fields, summed over the pass by pbr_last_pass_stats.
+enum StatField {
+    kStatCullKept = 0,        // culled passes: surviving point/spot lights of the culling unit
+    kStatCullTiles = 1,       // culled passes: 1 when the culling unit has geometry
+    kStatExactPixels = 2,     // geometry pixels whose light sum the exact path redid
+    kStatLightTerms = 3,      // (geometry pixel, light) terms the light loops evaluated
+    kStatGeometryPixels = 4,  // geometry pixels
+    kStatBackfaceTests = 5,   // balanced passes: (pixel, point light) back-face tests of pass 1
+    kStatsPerBlock = 6
+};
 constexpr int kBalMaxLights = 64;  // point lights per wave-balanced pass (one 64-bit live mask per pixel)
 
 struct LaunchArgs {

@@ -576,6 +576,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     // lives only in packed form (q2, pos2); the scalar views are rebuilt from it afterwards so the
     // loop does not carry two copies of the invariants.
     int kept_total = 0;
+    int bal_items = -1;  // wave-uniform: the balanced pass's live point-light items (statistics), -1 = not run
     m2 redo = m2{0, 0};
     f3x2 pos2 = p.pos;
     float ao_a = p.ao.x, ao_b = p.ao.y;
@@ -615,6 +616,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 // unscaled ones once more for the finish. launder() keeps the compiler from merging the
                 // rebuilds with the computation above (which would keep q2 live across the loop: it spilled).
                 const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, s.bal[wave_id], s.bal_light, prof);
+                bal_items = wave_live_items(bm);
                 launder(p);
                 q2 = pair_invariants(p, ps, fast2);
                 faithful_scale(q2);
@@ -673,6 +675,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                       vb && gb.pairs_aligned);
                 };
                 const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, s.bal[wave_id], s.bal_light, prof);
+                bal_items = wave_live_items(bm);
                 q2 = pair_invariants(p, ps, fast2);
                 d2 = lighting_fast<false, true, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
                                                              kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
@@ -692,13 +695,23 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     f3 da = lane(d2, 0), db = lane(d2, 1);
     const bool need_a = ga && on(redo.x), need_b = gb_ && on(redo.y);
     // Statistics, one record per wave (kStatsPerBlock ints at slot tile * 4 + wave): culling survivors and
-    // whether the wave has geometry (culled passes), and the pixels it sends to the exact path.
+    // whether the wave has geometry (culled passes), the pixels it sends to the exact path, and the work the
+    // light loops executed for its geometry pixels: light terms evaluated (every light of the pass in the
+    // uniform loop, the survivors of the wave's box under culling, the live items of the balanced lists) and
+    // the balanced pass-1 back-face tests.
     const int n_exact = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
+    const int geo_px = __popcll(lanes(ga)) + __popcll(lanes(gb_));
     if ((tid & 63) == 0 && tile_kept != nullptr) {
         const int64_t slot = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
-        tile_kept[kStatsPerBlock * slot] = CULL && wave_geometry ? kept_total : 0;
-        tile_kept[kStatsPerBlock * slot + 1] = CULL && wave_geometry ? 1 : 0;
-        tile_kept[kStatsPerBlock * slot + 2] = n_exact;
+        const int n_ps = CULL ? kept_total : ps.n_point + ps.n_spot;
+        const int terms = !wave_geometry ? 0 : bal_items >= 0 ? bal_items + ps.n_dir * geo_px : (ps.n_dir + n_ps) * geo_px;
+        int32_t* st = tile_kept + kStatsPerBlock * slot;
+        st[kStatCullKept] = CULL && wave_geometry ? kept_total : 0;
+        st[kStatCullTiles] = CULL && wave_geometry ? 1 : 0;
+        st[kStatExactPixels] = n_exact;
+        st[kStatLightTerms] = terms;
+        st[kStatGeometryPixels] = geo_px;
+        st[kStatBackfaceTests] = wave_geometry && bal_items >= 0 ? ps.n_point * geo_px : 0;
     }
 #if PBR_BAL_PROFILE
     const long long t_b0 = (long long)__builtin_amdgcn_s_memtime();
@@ -858,11 +871,16 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
         lighting_exact<CULL>(q, q, pos, pos, need, false, lights, ps, s, tb, cull_enabled, e, unused);
         if (need) direct = e;
     }
+    const int geo_px = __syncthreads_count(geom);
     if (tid == 0 && tile_kept != nullptr) {  // this layout culls per block (32x8 pixels)
         const int64_t t = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-        tile_kept[kStatsPerBlock * t] = CULL && any_geometry ? kept_total : 0;
-        tile_kept[kStatsPerBlock * t + 1] = CULL && any_geometry ? 1 : 0;
-        tile_kept[kStatsPerBlock * t + 2] = n_exact;
+        int32_t* st = tile_kept + kStatsPerBlock * t;
+        st[kStatCullKept] = CULL && any_geometry ? kept_total : 0;
+        st[kStatCullTiles] = CULL && any_geometry ? 1 : 0;
+        st[kStatExactPixels] = n_exact;
+        st[kStatLightTerms] = any_geometry ? (ps.n_dir + (CULL ? kept_total : ps.n_point + ps.n_spot)) * geo_px : 0;
+        st[kStatGeometryPixels] = geo_px;
+        st[kStatBackfaceTests] = 0;
     }
     if (valid)
         store_pixel(fr, (int64_t)y * fr.out_stride + x,

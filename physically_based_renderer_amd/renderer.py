@@ -119,8 +119,6 @@ class GBuffer:
             raise ValueError("planes must be a (15, H, W) float32 tensor")
         if planes.stride(2) != 1:
             raise ValueError("planes rows must be contiguous")
-        if planes.stride(0) < planes.shape[1] * planes.stride(1) and planes.shape[1] > 1:
-            raise ValueError("planes must not overlap (stride(0) >= H * stride(1))")
         self.planes = planes
         self.height = planes.shape[1]
         self.width = planes.shape[2] if width is None else width
@@ -272,8 +270,8 @@ class ShadingContext:
         return out
 
     def pass_stats(self, stream=None) -> dict:
-        """pbr_last_pass_stats of the last pass as a dict (workgroups, culled, cull_tiles,
-        cull_tile_lights, exact_pixels)."""
+        """pbr_last_pass_stats of the last pass on ``stream`` as a dict (workgroups, culled, cull_tiles,
+        cull_tile_lights, exact_pixels, light_terms, geometry_pixels, backface_tests)."""
         st = N.PassStats()
         N.check(self.lib.pbr_last_pass_stats(self._h, ctypes.byref(st), ctypes.c_void_p(_stream_handle(stream))),
                 "pbr_last_pass_stats", self._h)

@@ -37,20 +37,46 @@ def test_flops_per_pixel_and_the_roof():
     assert f4 == pytest.approx(47 + 91 * 5.0 + 9 * 256 / 128)
 
 
-def test_pmc_lookup_is_keyed_by_workload_and_mode():
+def test_pmc_lookup_is_keyed_by_workload_and_mode(tmp_path):
     summary = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+    head = N.kernel_sources_sha()
     for key in ("cfg3_3840x2160_64pt_ibl_chelsea", "cfg3_3840x2160_64pt_ibl_chelsea_faithful"):
         assert key in summary
-        traffic, busy = bench.load_pmc(key)
         e = summary[key]
-        assert traffic == e["hbm_bytes_per_launch"] and 0.5 < busy <= 1.0
-        # HBM traffic within 15 % of the algorithmic bytes: no re-reads of the planes (the faithful
-        # kernel's residue over 1.0 is one spilled 64-bit index per work-item)
+        traffic, busy, prov = bench.load_pmc(key)
+        assert prov["kernel_sources_sha"] == head
+        if e.get("kernel_sources_sha") == head:  # profiled at this revision of the kernels: quoted
+            assert traffic == e["hbm_bytes_per_launch"] and 0.5 < busy <= 1.0 and "stale" not in prov
+        else:  # a profile of other kernel sources is never quoted
+            assert traffic is None and busy is None and prov["stale"]
+        # HBM traffic within 15 % of the algorithmic bytes: no re-reads of the planes
         assert 0.95 < e["traffic_over_algorithmic"] < 1.15
         # the committed kernel trace agrees with the bench's own events within 2 %
         kt = e["kernel_trace"]
         assert abs(kt["mean_ms_timed_steps"] - kt["bench_avg_launch_ms"]) / kt["bench_avg_launch_ms"] < 0.02
-    assert bench.load_pmc("no_such_workload") == (None, None)
+    assert bench.load_pmc("no_such_workload")[:2] == (None, None)
+    # the stamp decides: the same entry quoted under this build's hash, refused under another
+    e = dict(summary["cfg3_3840x2160_64pt_ibl_chelsea_faithful"])
+    for sha, quoted in ((head, True), ("0" * 16, False)):
+        e["kernel_sources_sha"] = sha
+        p = tmp_path / f"s_{sha}.json"
+        p.write_text(json.dumps({"w": e}))
+        traffic, busy, prov = bench.load_pmc("w", str(p))
+        assert (traffic == e["hbm_bytes_per_launch"]) if quoted else (traffic is None and prov["stale"])
+
+
+def test_executed_flops_count_only_evaluated_terms():
+    """frac_executed's model: per geometry pixel the fixed part, 91 / 74 FLOP per evaluated point / directional
+    term, 8 per back-face test of the balanced lists, the range tests of culled passes."""
+    pc3 = S.scene_pass(S.CONFIGS[3])
+    px = 1000
+    full = {"geometry_pixels": px, "light_terms": 64 * px, "backface_tests": 0, "culled": 0, "cull_tiles": 0}
+    assert bench.executed_flops_per_pixel(pc3, full, px) == bench.flops_per_pixel(pc3) == 5958
+    half = dict(full, light_terms=32 * px, backface_tests=64 * px)  # balanced: half the terms live
+    assert bench.executed_flops_per_pixel(pc3, half, px) == 27 + 20 + 87 + 91 * 32 + 8 * 64
+    pc4 = S.scene_pass(S.CONFIGS[4])
+    culled = {"geometry_pixels": px, "light_terms": 5 * px, "backface_tests": 0, "culled": 1, "cull_tiles": 8}
+    assert bench.executed_flops_per_pixel(pc4, culled, px) == pytest.approx(47 + 91 * 5 + 9 * 256 * 8 / px, abs=0.01)
 
 
 @pytest.mark.parametrize("kind", ["auto", "port"])

@@ -106,6 +106,12 @@ def test_bench_multi_rank_rehearsal(gpu):
     gp = d["gathered_frame_parity"]  # sampled rows of every band against the CPU oracle
     assert gp["rows_checked"] == 4 * 8 and gp["parity_max_code_diff"] <= 1
     assert d["shade_ms"] > 0 and d["gather_ms"] > 0
+    # the scaling anchor: rank 0's own band (identical per-rank geometry at every N) shaded alone
+    a = d["scale_anchor"]
+    assert a["workload"] == d["config"]["workload"] + "_band64" or a["workload"].endswith("_band64")
+    assert a["px_per_step"] == 8192 * 64 and a["output"] == "rgba8" and a["mode"] == d["mode"]
+    assert d["per_rank_mpix_s"] == pytest.approx(d["value"] / 4, abs=0.01)
+    assert d["efficiency_vs_anchor"] == pytest.approx(d["per_rank_mpix_s"] / a["value"], rel=1e-3)
 
 
 def _bench_torchrun(nproc, extra, timeout=600):
@@ -151,3 +157,26 @@ def test_bench_config5_one_gpu_is_the_per_rank_workload(gpu):
     assert d["config"]["width"] == 8192 and d["config"]["height"] == 1024 and d["config"]["rows_per_rank"] == 1024
     assert d["output"] == "rgba8" and d["gather_checksums_match"] is True and d["process_group"] is None
     assert d["cpu_baseline"]["kind"] == "port" and d["parity_max_code_diff"] <= 1
+
+
+def test_bench_default_line_carries_anchor_and_executed_roofline(gpu):
+    """`bench.py --gpus 1` (config 3): the line carries the scaling anchor -- one rank's config-5 band of
+    --rows-per-rank rows, RGBA8, the same mode -- and both roofline fractions, the executed one counting only
+    the terms the pass evaluated (the wave-balanced lists skip back-facing ones)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup",
+                        "1", "--ramp-ms", "0", "--no-cpu-baseline", "--rows-per-rank", "64"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["config"]["workload"] == "cfg3_3840x2160_64pt_ibl_chelsea" and d["n_gpus"] == 1
+    a = d["scale_anchor"]
+    assert a["workload"] == "cfg5_8192x8192_64pt_ibl_rowbands_band64" or a["workload"].endswith("_band64")
+    assert a["px_per_step"] == 8192 * 64 and a["output"] == "rgba8" and a["value"] > 0 and a["shade_ms"] > 0
+    rf = d["roofline"]
+    assert rf["bound"] == "mfma" and rf["flop_per_px"] == 5958
+    st = rf["pass_stats"]
+    # nearly every wave is lean and builds the lists (64 back-face tests per pixel); the rest run the uniform loop
+    assert st["geometry_pixels"] == 3840 * 2160 and 0.99 * 64 * 3840 * 2160 <= st["backface_tests"] <= 64 * 3840 * 2160
+    assert 0.3 * 64 * 3840 * 2160 < st["light_terms"] < 0.7 * 64 * 3840 * 2160
+    assert rf["executed_flop_per_px"] < rf["flop_per_px"] and 0 < rf["frac_executed"] < rf["frac"]
+    assert rf["pmc"]["kernel_sources_sha"] and (rf["traffic"] is None) == bool(rf["pmc"].get("stale"))

@@ -1,0 +1,173 @@
+"""One context, several streams: the device light-slot ring and per-stream statistics (pbr_context.hip).
+
+The reference never lets frame k+1's constants overwrite frame k's while the GPU reads them: it cycles a 3-deep
+FrameResource ring guarded by fences (FrameResource.h:111-140, PBRApp.cpp:220-243). The C ABI promises the same
+across streams (include/pbr/pbr_shade.h): every pbr_set_pass uploads into its own device slot, a pass reads the
+slot of the pbr_set_pass before it (waiting stream-side for an upload made on another stream), and a slot is
+overwritten only after the queued passes that read it. These tests alternate two different passes on two
+streams with no host synchronisation and require every frame to carry the bits of its pass shaded alone.
+
+Also here: the executed-work statistics (pbr_pass_stats.light_terms / geometry_pixels / backface_tests) that
+bench.py's frac_executed counts, checked against host counts of the same terms.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from physically_based_renderer_amd import _native as N
+from physically_based_renderer_amd import scenes as S
+from physically_based_renderer_amd.renderer import GBuffer, PassConstants, ShadingContext
+
+pytestmark = pytest.mark.gpu
+
+FRAMES = 50
+
+
+def _with(pc, **kw):
+    return PassConstants(**{**pc.__dict__, **kw})
+
+
+def _two_passes():
+    """Config 3's 64 point lights (exact, the default mode: balanced exact lists) and a different set of 48 in
+    the faithful mode (balanced faithful lists): different slots, kernels and light counts."""
+    cfg = S.CONFIGS[3].with_size(1024, 512)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pa = S.scene_pass(cfg)
+    rng = np.random.default_rng(7)
+    lb = pa.light_array()[:48].copy()
+    lb[:, 8:11] = np.stack([rng.uniform(-20, 20, 48), rng.uniform(-20, 20, 48), rng.uniform(-20, 0, 48)], 1)
+    lb[:, 0:3] = rng.uniform(0, 100, (48, 3))
+    pb = _with(pa, num_point_lights=48, lights_array=lb, flags=int(pa.flags) | N.PBR_FLAG_FAITHFUL)
+    return planes, pa, pb
+
+
+def _solo(ctx, gb, pc, env):
+    ctx.set_pass(pc)
+    ctx.set_env_map(env)
+    out = ctx.shade(gb)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), ctx.pass_stats()
+
+
+def test_alternating_passes_on_two_streams_without_host_sync(gpu, env_map):
+    planes, pa, pb = _two_passes()
+    gb = GBuffer.from_host(planes, gpu)
+    with ShadingContext(0) as ctx:
+        want_a, st_a = _solo(ctx, gb, pa, env_map)
+        want_b, st_b = _solo(ctx, gb, pb, env_map)
+        assert not O.bit_equal(want_a, want_b).all()
+        streams = [torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)]
+        outs = [torch.empty((gb.height, gb.width, 4), dtype=torch.float32, device=gpu) for _ in range(FRAMES)]
+        torch.cuda.synchronize()
+        for k in range(FRAMES):  # frame k: pass A on stream 0 (even k), pass B on stream 1 (odd k)
+            s = streams[k % 2]
+            ctx.set_pass(pa if k % 2 == 0 else pb, stream=s)
+            ctx.shade(gb, outs[k], stream=s)
+        # statistics are per stream: each stream's last pass, never a mix of both
+        got_a = ctx.pass_stats(streams[0])
+        got_b = ctx.pass_stats(streams[1])
+        torch.cuda.synchronize()
+        bad = [k for k in range(FRAMES)
+               if not O.bit_equal(outs[k].cpu().numpy(), want_a if k % 2 == 0 else want_b).all()]
+        assert not bad, f"frames {bad} differ from their pass shaded alone"
+        for got, want in ((got_a, st_a), (got_b, st_b)):
+            assert got == want
+
+
+def test_set_pass_on_one_stream_shade_on_another(gpu, env_map):
+    """pbr_set_pass queued on stream 0 behind a long pass, then shaded on stream 1: the shade waits for the
+    upload (stream-side) instead of reading the previous slot or a half-copied one."""
+    planes, pa, pb = _two_passes()
+    gb = GBuffer.from_host(planes, gpu)
+    with ShadingContext(0) as ctx:
+        want_b, _ = _solo(ctx, gb, pb, env_map)
+        ctx.set_pass(pa)
+        s0, s1 = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+        busy = [torch.empty((gb.height, gb.width, 4), dtype=torch.float32, device=gpu) for _ in range(8)]
+        out = torch.empty_like(busy[0])
+        torch.cuda.synchronize()
+        for o in busy:  # keep stream 0 busy so its later upload is still queued when stream 1 launches
+            ctx.shade(gb, o, stream=s0)
+        ctx.set_pass(pb, stream=s0)
+        ctx.shade(gb, out, stream=s1)
+        torch.cuda.synchronize()
+        assert O.bit_equal(out.cpu().numpy(), want_b).all()
+
+
+def _host_dots(planes, lights):
+    """(N . l, |N|_1 |l|_1) per (pixel, point light) in fp64, l = light position - P."""
+    p = planes[0:3].reshape(3, -1).T.astype(np.float64)
+    n = planes[3:6].reshape(3, -1).T.astype(np.float64)
+    lp = lights[:, 8:11].astype(np.float64)
+    l = lp[None, :, :] - p[:, None, :]
+    dots = np.einsum("pk,plk->pl", n, l)
+    scale = np.abs(n).sum(1)[:, None] * np.abs(l).sum(2)
+    return dots, scale
+
+
+def test_light_terms_uniform_balanced_and_culled(gpu, env_map):
+    import os
+
+    cfg = S.CONFIGS[3].with_size(512, 128)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    gb = GBuffer.from_host(planes, gpu)
+    px = cfg.width * cfg.height
+    n = pc.num_point_lights
+    old = os.environ.get("PBR_BALANCED_MIN")
+    try:
+        os.environ["PBR_BALANCED_MIN"] = "0"
+        with ShadingContext(0) as ctx:  # uniform loop: every light for every pixel
+            _, st = _solo(ctx, gb, pc, env_map)
+        assert st["geometry_pixels"] == px and st["light_terms"] == n * px and st["backface_tests"] == 0
+        os.environ["PBR_BALANCED_MIN"] = "1"
+        with ShadingContext(0) as ctx:
+            for mode in (0, N.PBR_FLAG_FAITHFUL):
+                _, st = _solo(ctx, gb, _with(pc, flags=int(pc.flags) | mode), env_map)
+                # lean waves (nearly all) build the lists: n back-face tests per pixel; a wave with a pixel outside
+                # the lean conditions runs the uniform loop over all n lights instead
+                assert st["geometry_pixels"] == px and st["backface_tests"] % n == 0
+                uniform_px = px - st["backface_tests"] // n
+                assert 0 <= uniform_px <= px // 20 and uniform_px % 128 == 0
+                # the list keeps every front-facing term and drops every clearly back-facing one (the test is
+                # conservative by 2^-18 |N|_1 B_j)
+                dots, scale = _host_dots(planes, pc.light_array())
+                must_live = int((dots > 1e-5 * scale).sum())
+                may_live = int((dots >= -1e-3 * scale).sum())
+                print(f"mode {mode}: live terms {st['light_terms']} in [{must_live}, {may_live}] of {n * px}, "
+                      f"{uniform_px} px in uniform waves")
+                assert must_live <= st["light_terms"] <= may_live + n * uniform_px
+    finally:
+        if old is None:
+            del os.environ["PBR_BALANCED_MIN"]
+        else:
+            os.environ["PBR_BALANCED_MIN"] = old
+    # tiled culling: each wave (64x2 pixels, all geometry here) evaluates its survivors for all 128 pixels
+    cfg4 = S.CONFIGS[4].with_size(1024, 256)
+    p4, _ = S.fill_gbuffer_host(cfg4)
+    pc4 = S.scene_pass(cfg4)
+    with ShadingContext(0) as ctx:
+        ctx.set_pass(pc4)
+        ctx.shade(GBuffer.from_host(p4, gpu))
+        st = ctx.pass_stats()
+    if os.environ.get("PBR_PIXELS_PER_THREAD") != "1":
+        assert st["light_terms"] == 128 * st["cull_tile_lights"]
+    assert st["geometry_pixels"] == cfg4.width * cfg4.height and st["culled"] == 1
+
+
+def test_geometry_pixels_follow_the_coverage_plane(gpu):
+    cfg = S.CONFIGS[1]  # the sphere over the sky
+    planes, cov = S.fill_gbuffer_host_coverage(cfg)
+    pc = S.scene_pass(cfg)
+    from physically_based_renderer_amd import envmap
+
+    with ShadingContext(0) as ctx:
+        ctx.set_pass(pc)
+        ctx.set_sky_map(envmap.procedural_sky_rgba16(64, 32))
+        ctx.shade_frame(GBuffer.from_host(planes, gpu), coverage=torch.from_numpy(cov).to(gpu))
+        st = ctx.pass_stats()
+    geo = int((cov != 0).sum())
+    assert 0 < geo < cfg.width * cfg.height
+    assert st["geometry_pixels"] == geo
+    assert st["light_terms"] == (pc.num_dir_lights + pc.num_point_lights + pc.num_spot_lights) * geo

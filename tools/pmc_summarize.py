@@ -15,6 +15,8 @@ import sys
 
 N_SIMD = 256 * 4  # MI355X: 256 CUs x 4 SIMDs
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from physically_based_renderer_amd._native import kernel_sources_sha  # noqa: E402
 
 
 def find(pattern):
@@ -65,6 +67,8 @@ def main():
         "valu_issue_busy": counters["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / (counters["GRBM_GUI_ACTIVE"] / 8),
         "source": f"profiles/{dst_tag}/pmc_*_{workload}.csv (rocprofv3 --pmc, separate passes, bench.py --steps 5)",
         "kernel_revision": revision,
+        # bench.py quotes traffic / valu_issue_busy only while the kernel sources still hash to this
+        "kernel_sources_sha": kernel_sources_sha(),
     }
     # Kernel trace of the bench run itself: mean launch time over the timed steps (the last K launches;
     # the clock-ramp and warm-up launches come first) next to the bench's own HIP-event average.
@@ -77,10 +81,13 @@ def main():
     for line in open(os.path.join(src, "kt.log")):
         if line.startswith("{"):
             bench = json.loads(line)
+    # launch order of bench.py: clock ramp, warm-up steps, the K timed steps, then (exact leg, scale anchor)
     k = bench["steps"] if bench else len(durs)
+    first = bench["clock_ramp"]["launches"] + bench["warmup"] if bench else len(durs) - k
+    timed = durs[first:first + k]
     entry["kernel_trace"] = {
         "launches": len(durs), "mean_ms_all": sum(durs) / len(durs),
-        "mean_ms_timed_steps": sum(durs[-k:]) / k, "timed_steps": k,
+        "mean_ms_timed_steps": sum(timed) / len(timed), "timed_steps": len(timed), "first_timed_launch": first,
         "bench_avg_launch_ms": bench["roofline"]["avg_launch_ms"] if bench else None,
         "bench_value": bench["value"] if bench else None,
     }
