@@ -359,14 +359,14 @@ __device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArg
     if (vector_load) {  // both pixels exist and the pair is 8-byte aligned in every plane
 #pragma unroll
         for (int i = 0; i < 15; ++i) {
-            if ((i == 11 && !APPLY_AO) || (i >= 12 && !F0_PLANE)) continue;
+            if (i == 11 || (i >= 12 && !F0_PLANE)) continue;  // AO: read at the finish (load_ao_pair)
             const float2 t = *reinterpret_cast<const float2*>(gb.plane[i] + ia);
             v[i] = v2{t.x, t.y};
         }
     } else {
 #pragma unroll
         for (int i = 0; i < 15; ++i) {
-            if ((i == 11 && !APPLY_AO) || (i >= 12 && !F0_PLANE)) continue;
+            if (i == 11 || (i >= 12 && !F0_PLANE)) continue;  // AO: read at the finish (load_ao_pair)
             v[i] = v2{gb.plane[i][ia], gb.plane[i][ib]};
         }
     }
@@ -376,7 +376,7 @@ __device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArg
     p.albedo = f3x2{v[6], v[7], v[8]};
     p.metallic = v[9];
     p.roughness = v[10];
-    p.ao = APPLY_AO ? v[11] : splat(1.0f);
+    p.ao = splat(1.0f);  // PBR_FLAG_APPLY_AO: load_ao_pair after the light loop
     if (F0_PLANE) {  // Default.hlsl:92
         p.f0 = f3x2{v[12], v[13], v[14]};
     } else {  // F0 = lerp(g_FresnelR0, diffuseAlbedo, metallic)  (Default.hlsl:94-95): x + s*(y - x)
@@ -579,7 +579,6 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     int bal_items = -1;  // wave-uniform: the balanced pass's live point-light items (statistics), -1 = not run
     m2 redo = m2{0, 0};
     f3x2 pos2 = p.pos;
-    float ao_a = p.ao.x, ao_b = p.ao.y;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
     bool faithful_wave = false;  // wave-uniform: the faithful loop ran, so the finish may be faithful too
     if (wave_geometry) {  // wave-uniform
@@ -597,7 +596,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             p.f0.y.x <= 1.0f && p.f0.z.x <= 1.0f && p.f0.x.y <= 1.0f && p.f0.y.y <= 1.0f && p.f0.z.y <= 1.0f &&
             p.f0.x.x >= 0.0f && p.f0.y.x >= 0.0f && p.f0.z.x >= 0.0f && p.f0.x.y >= 0.0f && p.f0.y.y >= 0.0f &&
             p.f0.z.y >= 0.0f;
-        faithful_wave = ps.faithful && lanes(!faithful_lane) == 0;
+        // BAL == 2 kernels shade exact passes only (host: PassArgs::balanced): no faithful code is compiled in.
+        faithful_wave = BAL != 2 && ps.faithful && lanes(!faithful_lane) == 0;
         if (CULL && faithful_wave && ps.faithful == 2)
             faithful_wave = wave_light_terms(lights, ps, wb, cull_enabled) <= kFaithfulMaxTerms;
         const bool lean_wave = lanes(!lean_lane) == 0;
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 pos2 = p.pos;
 #if PBR_BAL_PROFILE
                 const v2 dep = dot3(q2.n, q2.v);
-                if (dep.x == 12345.0f) ao_a = 0.5f;
+                if (dep.x == 12345.0f) pos2.x.x = 0.5f;
                 BAL_PROF_ADD(8, (long long)__builtin_amdgcn_s_memtime() - t_l1);
 #endif
             } else {
@@ -644,7 +644,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 if (!CULL) faithful_unscale(q2);
 #if PBR_BAL_PROFILE
                 const v2 dep = d2.x + d2.y;
-                if (dep.x == 12345.0f) ao_a = 0.5f;
+                if (dep.x == 12345.0f) pos2.x.x = 0.5f;
                 BAL_PROF_ADD(12, (long long)__builtin_amdgcn_s_memtime() - t_u0);
 #endif
             }
@@ -681,8 +681,6 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                              kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
                                                              prof);
                 reload();
-                ao_a = p.ao.x;
-                ao_b = p.ao.y;
                 q2 = pair_invariants(p, ps, fast2);
                 pos2 = p.pos;
             } else {
@@ -739,6 +737,20 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const int ln = lane_id_fresh();
     const int sx = blockIdx.x * kTileW + 2 * (ln & 31);
     const int64_t orow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
+    // PBR_FLAG_APPLY_AO: the AO pair is read only now, for the finish (Default.hlsl:150 ambient * AO): a value
+    // loaded at entry would be live across the light loops (it was the one spilled value of the AO kernels).
+    float ao_a = 1.0f, ao_b = 1.0f;
+    if (APPLY_AO) {
+        const int64_t arow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
+        if (vb && gb.pairs_aligned) {
+            const float2 t = *reinterpret_cast<const float2*>(gb.plane[11] + arow);
+            ao_a = t.x;
+            ao_b = t.y;
+        } else {
+            if (va) ao_a = gb.plane[11][arow];
+            if (vb) ao_b = gb.plane[11][arow + 1];
+        }
+    }
     if (va)
         store_pixel(fr, orow, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
                                  : sky_pixel(ua.n, ps, fr.sky, !exact_only));
