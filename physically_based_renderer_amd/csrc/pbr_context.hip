@@ -659,3 +659,8 @@ int pbr_last_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream) {
 extern "C" int pbr_debug_bal_profile(unsigned long long* out8, int reset) {
     return pbr::debug_bal_profile(out8, reset != 0) == hipSuccess ? 0 : -1;
 }
+
+// Development: per-wave clock stamps of a PBR_WAVE_TIMELINE build into a device buffer of cap_waves * 8 words.
+extern "C" int pbr_debug_wave_timeline(void* dev_buf, long long cap_waves) {
+    return pbr::debug_wave_timeline(static_cast<unsigned long long*>(dev_buf), cap_waves) == hipSuccess ? 0 : -1;
+}

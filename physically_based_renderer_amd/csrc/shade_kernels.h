@@ -84,6 +84,7 @@ int64_t shade_tile_count(int width, int height, int pixels_per_thread);
 // Statistics records per tile: one per wave in the pair layout, one per workgroup in the one-pixel layout.
 int shade_stat_slots_per_tile(int pixels_per_thread);
 hipError_t debug_bal_profile(unsigned long long* out8, bool reset);  // PBR_BAL_PROFILE builds only
+hipError_t debug_wave_timeline(unsigned long long* buf, long long cap);  // PBR_WAVE_TIMELINE builds only
 hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream);
 
 }  // namespace pbr

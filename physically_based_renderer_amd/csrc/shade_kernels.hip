@@ -32,6 +32,42 @@
 
 namespace pbr {
 
+#ifndef PBR_WAVE_TIMELINE
+#define PBR_WAVE_TIMELINE 0  // development build: per-wave clock stamps of the pair kernels (pbr_debug_wave_timeline)
+#endif
+#if PBR_WAVE_TIMELINE
+// kTlWords per wave (wave = block * 4 + wave in block): [0] HW_ID | XCC_ID << 32, [1] entry, [2] G-buffer pair
+// arrived, [3] light loops start, [4] light loops end, [5] stores issued (s_memrealtime, 100 MHz, one clock for
+// the whole chip), [6] / [7] s_memtime (shader clock) at entry / at the end. Lane 0 stores them (vector stores).
+constexpr int kTlWords = 8;
+static __device__ unsigned long long* g_wave_tl;
+static __device__ long long g_wave_tl_cap;
+#define TL_RT(i_) (tl[i_] = (unsigned long long)__builtin_amdgcn_s_memrealtime())
+#define TL_BEGIN()                                                                                           \
+    unsigned long long tl[kTlWords];                                                                         \
+    TL_RT(1);                                                                                                \
+    tl[6] = (unsigned long long)__builtin_amdgcn_s_memtime();                                                \
+    tl[0] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                                            \
+            ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32)
+#define TL_LOADED()                                      \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    TL_RT(2)
+#define TL_END(wv_)                                                                     \
+    do {                                                                                \
+        TL_RT(5);                                                                       \
+        tl[7] = (unsigned long long)__builtin_amdgcn_s_memtime();                       \
+        const long long w_ = (wv_);                                                     \
+        if ((threadIdx.x & 63) == 0 && g_wave_tl != nullptr && w_ < g_wave_tl_cap) {    \
+            for (int i_ = 0; i_ < kTlWords; ++i_) g_wave_tl[w_ * kTlWords + i_] = tl[i_]; \
+        }                                                                               \
+    } while (0)
+#else
+#define TL_BEGIN()
+#define TL_LOADED()
+#define TL_RT(i_)
+#define TL_END(wv_)
+#endif
+
 namespace {
 
 constexpr int kTileW = 64;  // pixels; 32 work-items x 2 pixels
@@ -521,6 +557,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                             int32_t* __restrict__ tile_kept,
                                                             bool exact_only) {
     __shared__ Lds s;
+    TL_BEGIN();
 #if PBR_BAL_PROFILE
     const long long t_entry = (long long)__builtin_amdgcn_s_memtime();
     unsigned long long* bal_prof = s.prof[__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6];
@@ -551,6 +588,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const bool ok_b = !exact_only && ps.eye_ok && fast_window_ok(pb, lane(p.n, 1), lane(p.albedo, 1), lane(p.f0, 1),
                                                     p.metallic.y, p.roughness.y);
     const m2 fast2 = mask2(ok_a, ok_b);
+    TL_LOADED();
 
     PixelInvariants2 q2 = pair_invariants(p, ps, fast2);
 
@@ -581,6 +619,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     f3x2 pos2 = p.pos;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
     bool faithful_wave = false;  // wave-uniform: the faithful loop ran, so the finish may be faithful too
+    TL_RT(3);
     if (wave_geometry) {  // wave-uniform
         // Wave-uniform choice of the light loop.
         const v2 nn = dot3(p.n, p.n);
@@ -689,6 +728,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         } else
             d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
     }
+    TL_RT(4);
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
     f3 da = lane(d2, 0), db = lane(d2, 1);
     const bool need_a = ga && on(redo.x), need_b = gb_ && on(redo.y);
@@ -757,6 +797,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     if (vb)
         store_pixel(fr, orow + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
                                       : sky_pixel(ub.n, ps, fr.sky, !exact_only));
+    TL_END(((long long)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id);
 }
 
 // ---- One pixel per work-item (32x8 tiles) ---------------------------------------------------------
@@ -968,6 +1009,28 @@ hipError_t debug_bal_profile(unsigned long long* out8, bool reset) {
 }
 
 #endif
+
+// Development builds with PBR_WAVE_TIMELINE: point this translation unit's kernels at a device buffer of
+// cap * kTlWords words (nullptr: off).
+#if PBR_BAL_TU
+hipError_t debug_wave_timeline_bal(unsigned long long* buf, long long cap) {
+#else
+hipError_t debug_wave_timeline_bal(unsigned long long* buf, long long cap);
+hipError_t debug_wave_timeline(unsigned long long* buf, long long cap) {
+#endif
+#if PBR_WAVE_TIMELINE
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_wave_tl), &buf, sizeof(buf));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_wave_tl_cap), &cap, sizeof(cap));
+#if !PBR_BAL_TU && PBR_SPLIT_BAL
+    if (e == hipSuccess) e = debug_wave_timeline_bal(buf, cap);
+#endif
+    return e;
+#else
+    (void)buf;
+    (void)cap;
+    return hipErrorNotSupported;
+#endif
+}
 
 #if !PBR_BAL_TU
 __global__ void decode_unorm16_kernel(const uint16_t* __restrict__ src, float4* __restrict__ dst, int n) {
