@@ -87,6 +87,7 @@ struct pbr_context {
     int balanced_min = -1;
     bool points_flag_ok = false;  // pbr_set_pass: every point light inside the fast-path window
     int pixels_per_thread = 2;  // kernel layout: packed pixel pairs (measured faster); PBR_PIXELS_PER_THREAD=1 overrides
+    bool lean = true;  // uniform-loop passes without a sky pass use the lean pair kernel (PBR_LEAN=0: off)
     std::string last_error;
     std::mutex mu;
 };
@@ -228,6 +229,7 @@ int pbr_context_create(int device, pbr_context** out_ctx) {
     ctx->device = device;
     if (const char* e = std::getenv("PBR_PIXELS_PER_THREAD")) ctx->pixels_per_thread = std::atoi(e) == 1 ? 1 : 2;
     if (const char* e = std::getenv("PBR_BALANCED_MIN")) ctx->balanced_min = std::atoi(e);
+    if (const char* e = std::getenv("PBR_LEAN")) ctx->lean = std::atoi(e) != 0;
     DeviceGuard g(device);
     if (!g.ok) {
         delete ctx;
@@ -543,6 +545,8 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
         st.slots = slots;
         st.culled = cull;
         a.tile_kept = st.d_stats;
+        // The lean pair kernel: uniform light loops (no balanced lists), no sky pass, the fast paths enabled.
+        a.lean = ctx->lean && a.pixels_per_thread == 2 && a.ps.balanced == 0 && !fr->coverage && !a.exact_only;
     }
     // Order the pass after the writes of what it reads (lights, textures) made on other streams.
     const bool reads_lights = ctx->cur_slot >= 0 && a.ps.n_dir + a.ps.n_point + a.ps.n_spot > 0;

@@ -76,6 +76,9 @@ struct LaunchArgs {
     bool f0_plane, apply_ao, cull;
     bool exact_only;  // PBR_FLAG_EXACT_ONLY: skip the exact fast path (validation mode)
     int pixels_per_thread;  // 1 (32x8 tiles) or 2 (64x8 tiles, packed pairs)
+    // Shade with the lean pair kernel (uniform-loop passes without a sky pass or EXACT_ONLY, pixels_per_thread 2;
+    // tile_kept required): shade_lean_kernel.
+    bool lean;
 };
 
 hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);

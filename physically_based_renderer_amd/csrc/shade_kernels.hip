@@ -52,6 +52,7 @@ static __device__ long long g_wave_tl_cap;
 #define TL_LOADED()                                      \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
     TL_RT(2)
+#define TL_FLAGS(f_) (tl[0] |= (unsigned long long)(f_) << 48)  // bits 48+: kernel-specific wave flags
 #define TL_END(wv_)                                                                     \
     do {                                                                                \
         TL_RT(5);                                                                       \
@@ -63,6 +64,7 @@ static __device__ long long g_wave_tl_cap;
     } while (0)
 #else
 #define TL_BEGIN()
+#define TL_FLAGS(f_)
 #define TL_LOADED()
 #define TL_RT(i_)
 #define TL_END(wv_)
@@ -73,6 +75,9 @@ namespace {
 constexpr int kTileW = 64;  // pixels; 32 work-items x 2 pixels
 #ifndef PBR_X2_MIN_WAVES
 #define PBR_X2_MIN_WAVES 4  // waves per SIMD the packed kernel is register-allocated for
+#endif
+#ifndef PBR_LEAN_MIN_WAVES
+#define PBR_LEAN_MIN_WAVES 4  // waves per SIMD the lean pair kernel is register-allocated for
 #endif
 constexpr int kTileH = 8;
 constexpr int kBlock = 256;
@@ -800,6 +805,184 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     TL_END(((long long)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id);
 }
 
+// ---- Lean pair kernel ------------------------------------------------------------------------------------------
+// shade_tile_kernel's register allocation is the maximum over every path it carries, and its exact re-pass runs
+// with the fast path's state (invariants, positions, sums) still live around it. shade_lean_kernel is the same
+// per-wave choice of fast loops for uniform-loop passes (no balanced lists) without a sky pass, but it finishes
+// and stores every pixel the fast loop settled first, and only then re-passes the pixels the loop sent to the
+// exact path, one at a time, reading each back from the G-buffer and evaluating it with the IEEE sequences
+// (shade_pixel_exact; the finish of its wave: faithful in a faithful wave). Nothing of the fast path is live
+// there, so the rare path does not raise the register peak of the loops, and the faithful-only instantiation
+// (FAITHFUL: the pass has PBR_FLAG_FAITHFUL) carries no faithful code in the exact-mode one. Frames and pass
+// statistics are bit-identical to shade_tile_kernel's (tests/test_gpu_lean.py).
+
+// One pixel (G-buffer index `idx`) with the compiler's IEEE sequences: V, the BRDF invariants, the light sum in
+// the reference's order (lighting_exact_wave: every light, no culling) and the finish (faithful_finish: the
+// faithful wave's finish of a re-passed pixel). Wave-uniform call; lanes with !need return zeros.
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO>
+__device__ __forceinline__ float4 shade_pixel_exact(const GBufferArgs& gb, const PassArgs& ps,
+                                                    const float4* __restrict__ lights, const float4* __restrict__ env,
+                                                    int64_t idx, bool need, bool faithful_finish) {
+    idx = need ? idx : 0;
+    const f3 pos = mk3(gb.plane[0][idx], gb.plane[1][idx], gb.plane[2][idx]);
+    const f3 n = mk3(gb.plane[3][idx], gb.plane[4][idx], gb.plane[5][idx]);
+    const f3 albedo = mk3(gb.plane[6][idx], gb.plane[7][idx], gb.plane[8][idx]);
+    const float metallic = gb.plane[9][idx], roughness = gb.plane[10][idx];
+    const float ao = APPLY_AO ? gb.plane[11][idx] : 1.0f;
+    // F0 exactly as load_pair forms it (Default.hlsl:92-95).
+    const f3 f0 = F0_PLANE ? mk3(gb.plane[12][idx], gb.plane[13][idx], gb.plane[14][idx])
+                           : mk3(ps.fresnel_r0[0] + metallic * (albedo.x - ps.fresnel_r0[0]),
+                                 ps.fresnel_r0[1] + metallic * (albedo.y - ps.fresnel_r0[1]),
+                                 ps.fresnel_r0[2] + metallic * (albedo.z - ps.fresnel_r0[2]));
+    const f3 eye = mk3(ps.eye[0], ps.eye[1], ps.eye[2]);
+    const PixelInvariants q = make_invariants(n, normalize3(sub3(eye, pos)), albedo, f0, metallic, roughness);
+    f3 d, unused;
+    lighting_exact_wave(q, q, pos, pos, need, false, lights, ps, d, unused);
+    return finish_pixel<AMBIENT, APPLY_AO>(q, ao, d, ps, env, false, faithful_finish);
+}
+
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, bool FAITHFUL>
+__global__ __launch_bounds__(kBlock, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBufferArgs gb, PassArgs ps,
+                                                            const float4* __restrict__ lights,
+                                                            const float4* __restrict__ env, FrameArgs fr,
+                                                            int32_t* __restrict__ tile_kept) {
+    load_libm_tables();  // powf tables -> LDS: the exact finish's gamma, spot cones, the faithful gamma's edges
+    __syncthreads();
+    TL_BEGIN();
+    const int tid = threadIdx.x;
+    const int wave_id = __builtin_amdgcn_readfirstlane(tid) >> 6;
+    const int64_t wave_global = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
+    const int xa = blockIdx.x * kTileW + 2 * (tid & 31);
+    const int y = blockIdx.y * kTileH + (tid >> 5);
+    const bool va = (xa < gb.width) && (y < gb.height);
+    const bool vb = (xa + 1 < gb.width) && (y < gb.height);
+    const int geo_px = __popcll(lanes(va)) + __popcll(lanes(vb));
+    if (geo_px == 0) {  // wholly outside the frame: nothing to shade, an empty statistics record
+        if ((tid & 63) == 0) {
+            int32_t* st = tile_kept + kStatsPerBlock * wave_global;
+            for (int i = 0; i < kStatsPerBlock; ++i) st[i] = 0;
+        }
+        return;
+    }
+    const int64_t row = (int64_t)y * gb.row_stride;
+    bool need_a, need_b;           // pixels for the IEEE path (the exact re-pass)
+    bool faithful_wave = false;    // wave-uniform
+    int kept_total = 0;
+    {
+        PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
+                                                 vb && gb.pairs_aligned);
+        // shade_pair_wave's per-wave choice of the light loop (BAL 0, every pixel geometry), unchanged.
+        const bool ok_a = ps.eye_ok && fast_window_ok(lane(p.pos, 0), lane(p.n, 0), lane(p.albedo, 0),
+                                                      lane(p.f0, 0), p.metallic.x, p.roughness.x);
+        const bool ok_b = ps.eye_ok && fast_window_ok(lane(p.pos, 1), lane(p.n, 1), lane(p.albedo, 1),
+                                                      lane(p.f0, 1), p.metallic.y, p.roughness.y);
+        const m2 fast2 = mask2(ok_a, ok_b);
+        TL_LOADED();
+        PixelInvariants2 q2 = pair_invariants(p, ps, fast2);
+        TileBounds wb{};
+        bool cull_enabled = false;
+        if (CULL) {  // the wave's box, as in shade_pair_wave (every pixel is geometry: no sky pass)
+            const f3 pa = lane(p.pos, 0), pb = lane(p.pos, 1);
+            const bool finite = (!va || (isfinite(pa.x) && isfinite(pa.y) && isfinite(pa.z))) &&
+                                (!vb || (isfinite(pb.x) && isfinite(pb.y) && isfinite(pb.z)));
+            const float big = 3.0e38f;
+            wb.mn[0] = uniform_f(wave_min(fminf(va ? pa.x : big, vb ? pb.x : big)));
+            wb.mn[1] = uniform_f(wave_min(fminf(va ? pa.y : big, vb ? pb.y : big)));
+            wb.mn[2] = uniform_f(wave_min(fminf(va ? pa.z : big, vb ? pb.z : big)));
+            wb.mx[0] = uniform_f(wave_max(fmaxf(va ? pa.x : -big, vb ? pb.x : -big)));
+            wb.mx[1] = uniform_f(wave_max(fmaxf(va ? pa.y : -big, vb ? pb.y : -big)));
+            wb.mx[2] = uniform_f(wave_max(fmaxf(va ? pa.z : -big, vb ? pb.z : -big)));
+            cull_enabled = lanes(!finite) == 0;
+        }
+        const v2 nn = dot3(p.n, p.n);
+        const bool lean_lane = ok_a && ok_b && nn.x <= 1.0f + 0x1p-20f && nn.y <= 1.0f + 0x1p-20f &&
+                               on(q2.f0_nonzero.x) && on(q2.f0_nonzero.y);
+        if (FAITHFUL) {
+            const bool faithful_lane =
+                ok_a && ok_b && p.albedo.x.x >= 0.0f && p.albedo.y.x >= 0.0f && p.albedo.z.x >= 0.0f &&
+                p.albedo.x.y >= 0.0f && p.albedo.y.y >= 0.0f && p.albedo.z.y >= 0.0f && p.f0.x.x <= 1.0f &&
+                p.f0.y.x <= 1.0f && p.f0.z.x <= 1.0f && p.f0.x.y <= 1.0f && p.f0.y.y <= 1.0f && p.f0.z.y <= 1.0f &&
+                p.f0.x.x >= 0.0f && p.f0.y.x >= 0.0f && p.f0.z.x >= 0.0f && p.f0.x.y >= 0.0f && p.f0.y.y >= 0.0f &&
+                p.f0.z.y >= 0.0f;
+            faithful_wave = lanes(!faithful_lane) == 0;
+            if (CULL && faithful_wave && ps.faithful == 2)
+                faithful_wave = wave_light_terms(lights, ps, wb, cull_enabled) <= kFaithfulMaxTerms;
+        }
+        const bool lean_wave = lanes(!lean_lane) == 0;
+        TL_RT(3);
+        m2 redo = m2{0, 0};
+        f3x2 d2;
+        if (faithful_wave) {
+            if (!CULL) faithful_scale(q2);
+            if (lean_wave)
+                d2 = lighting_fast<CULL, true, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+            else
+                d2 = lighting_fast<CULL, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+            if (!CULL) faithful_unscale(q2);
+        } else if (lean_wave) {
+            d2 = lighting_fast<CULL, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+        } else {
+            d2 = lighting_fast<CULL, false>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+        }
+        TL_RT(4);
+        {
+            need_a = va && on(redo.x);
+            need_b = vb && on(redo.y);
+            // Finish and store every pixel the fast loop settled.
+            const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
+            const int ln = lane_id_fresh();
+            const int sx = blockIdx.x * kTileW + 2 * (ln & 31);
+            const int64_t orow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
+            float ao_a = 1.0f, ao_b = 1.0f;
+            if (APPLY_AO) {
+                const int64_t arow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
+                if (vb && gb.pairs_aligned) {
+                    const float2 t = *reinterpret_cast<const float2*>(gb.plane[11] + arow);
+                    ao_a = t.x;
+                    ao_b = t.y;
+                } else {
+                    if (va) ao_a = gb.plane[11][arow];
+                    if (vb) ao_b = gb.plane[11][arow + 1];
+                }
+            }
+            if (va && !need_a)
+                store_pixel(fr, orow, finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, lane(d2, 0), ps, env, ok_a, faithful_wave));
+            if (vb && !need_b)
+                store_pixel(fr, orow + 1, finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, lane(d2, 1), ps, env, ok_b, faithful_wave));
+        }
+    }
+    const int n_exact = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
+    if ((tid & 63) == 0) {
+        const bool culled = CULL;
+        const int n_ps = culled ? kept_total : ps.n_point + ps.n_spot;
+        int32_t* st = tile_kept + kStatsPerBlock * wave_global;
+        st[kStatCullKept] = culled ? kept_total : 0;
+        st[kStatCullTiles] = culled ? 1 : 0;
+        st[kStatExactPixels] = n_exact;
+        st[kStatLightTerms] = (ps.n_dir + n_ps) * geo_px;
+        st[kStatGeometryPixels] = geo_px;
+        st[kStatBackfaceTests] = 0;
+    }
+    if (n_exact != 0) {  // wave-uniform, rare: the IEEE path, one pixel of the pair at a time
+        const int ln = lane_id_fresh();
+        const int rx = blockIdx.x * kTileW + 2 * (ln & 31);
+        const int ry = blockIdx.y * kTileH + 2 * wave_id + (ln >> 5);
+        const int64_t gi = (int64_t)ry * gb.row_stride + rx, oi = (int64_t)ry * fr.out_stride + rx;
+        if (lanes(need_a) != 0) {
+            const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO>(gb, ps, lights, env, gi, need_a,
+                                                                            faithful_wave);
+            if (need_a) store_pixel(fr, oi, c);
+        }
+        if (lanes(need_b) != 0) {
+            const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO>(gb, ps, lights, env, gi + 1, need_b,
+                                                                            faithful_wave);
+            if (need_b) store_pixel(fr, oi + 1, c);
+        }
+    }
+    TL_FLAGS((n_exact != 0 ? 1 : 0) | (FAITHFUL && !faithful_wave ? 2 : 0));
+    TL_END(wave_global);
+}
+
 // ---- One pixel per work-item (32x8 tiles) ---------------------------------------------------------
 // The same algorithm on the scalar fast path (pbr_device_math.h). Packing a pixel pair (above) halves
 // the instruction count but not the VALU cycles (a v_pk_fma_f32 issues in twice the cycles of a
@@ -1048,7 +1231,14 @@ static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
         dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
         if (!CULL && a.ps.balanced != 0)
             return launch_balanced<AMBIENT, F0_PLANE, APPLY_AO>(a, grid, stream);
-        else
+        if (a.lean) {  // uniform loops, no sky pass (shade_lean_kernel)
+            if (a.ps.faithful)
+                hipLaunchKernelGGL((shade_lean_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL, true>), grid, dim3(kBlock), 0,
+                                   stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept);
+            else
+                hipLaunchKernelGGL((shade_lean_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL, false>), grid, dim3(kBlock), 0,
+                                   stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept);
+        } else
             hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,
                                a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
     } else {

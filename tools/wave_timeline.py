@@ -27,7 +27,8 @@ TICK_NS = 10.0  # s_memrealtime: 100 MHz
 def analyse(tl: np.ndarray, name: str) -> dict:
     """tl: (waves, 8) uint64 stamps of one launch (rows of waves that never ran are zero)."""
     tl = tl[tl[:, 1] != 0]
-    hw, xcc = (tl[:, 0] & 0xFFFFFFFF).astype(np.int64), (tl[:, 0] >> 32).astype(np.int64)
+    hw, xcc = (tl[:, 0] & 0xFFFFFFFF).astype(np.int64), ((tl[:, 0] >> 32) & 0xFFFF).astype(np.int64)
+    flags = (tl[:, 0] >> 48).astype(np.int64)  # shade_lean_kernel: 1 = pixels re-passed, 2 = not a faithful wave
     t = tl[:, 1:6].astype(np.int64)
     t0 = t[:, 0].min()
     t = (t - t0) * TICK_NS / 1e3  # us from the first wave's entry
@@ -71,6 +72,14 @@ def analyse(tl: np.ndarray, name: str) -> dict:
                                "p90": round(float(np.percentile(gaps, 90)), 3) if gaps.size else None},
         "last_entry_us": round(float(entry.max()), 2),
         "first_round_entries_within_us": round(float(np.sort(entry)[min(len(entry) - 1, 4 * n_simd - 1)]), 3),
+        "wave_life_max_us": round(float(life.max()), 3),
+        # the waves that end last: when they entered and how long they lived
+        "last_to_end": [{"entry_us": round(float(entry[i]), 2), "life_us": round(float(life[i]), 2),
+                         "loop_us": round(float(loop1[i] - loop0[i]), 2), "after_loop_us": round(float(done[i] - loop1[i]), 2),
+                         "flags": int(flags[i])} for i in np.argsort(done)[-8:]],
+        "flagged": {str(f): {"waves": int((flags == f).sum()), "life_us_mean": round(float(life[flags == f].mean()), 2),
+                             "after_loop_us_mean": round(float((done - loop1)[flags == f].mean()), 2)}
+                    for f in np.unique(flags)},
         # chip-wide: waves per SIMD in each phase, per 1-us bin
         "timeline_per_simd": {k: [round(float(v) / n_simd, 2) for v in phase[k]] for k in phase},
     }
