@@ -816,14 +816,53 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 // (FAITHFUL: the pass has PBR_FLAG_FAITHFUL) carries no faithful code in the exact-mode one. Frames and pass
 // statistics are bit-identical to shade_tile_kernel's (tests/test_gpu_lean.py).
 
+// The IEEE light sum of ONE pixel (wave-uniform `q`, `pos`) with the wave's lanes splitting the lights: lane l
+// evaluates light base + l (point_or_spot_light / directional_light, the functions lighting_exact_wave calls),
+// and the terms are then added in light order from +0 -- directional, point, spot, as the reference's
+// ComputeLighting loops (LightingUtil.hlsl:176-199). An unlit light's term is +0, which leaves the sum as it is
+// (it starts at +0 and is never -0), exactly as lighting_exact_wave's skipped addition. One evaluation of a
+// light's sequence per 64 lights instead of one per light: a wave with a handful of pixels to re-pass finishes
+// in a fraction of the serial loop's time (those waves were the stragglers of short launches).
+__device__ __forceinline__ f3 lighting_exact_lanes(const PixelInvariants& q, f3 pos, const float4* __restrict__ lights,
+                                                   const PassArgs& ps) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int n = ps.n_dir + ps.n_point + ps.n_spot, sp_begin = ps.n_dir + ps.n_point;
+    f3 sum = mk3(0.0f, 0.0f, 0.0f);
+    for (int base = 0; base < n; base += 64) {
+        const int j = base + lane;
+        f3 t = mk3(0.0f, 0.0f, 0.0f);
+        bool unused = true;
+        if (j < n) {
+            const float4 r0 = lights[3 * j], r1 = lights[3 * j + 1], r2 = lights[3 * j + 2];
+            if (j < ps.n_dir) {
+                t = directional_light<false>(q, r0, r1, unused);
+            } else {
+                f3 c;
+                const bool lit = j >= sp_begin ? point_or_spot_light<true, false>(q, pos, r0, r1, r2, c, unused)
+                                               : point_or_spot_light<false, false>(q, pos, r0, r1, r2, c, unused);
+                if (lit) t = c;
+            }
+        }
+        const int cnt = min(64, n - base);
+        for (int k = 0; k < cnt; ++k) {
+            sum.x = sum.x + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.x), k));
+            sum.y = sum.y + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.y), k));
+            sum.z = sum.z + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.z), k));
+        }
+    }
+    return sum;
+}
+
 // One pixel (G-buffer index `idx`) with the compiler's IEEE sequences: V, the BRDF invariants, the light sum in
 // the reference's order (lighting_exact_wave: every light, no culling) and the finish (faithful_finish: the
 // faithful wave's finish of a re-passed pixel). Wave-uniform call; lanes with !need return zeros.
-template <int AMBIENT, bool F0_PLANE, bool APPLY_AO>
+// LANES: `idx` is wave-uniform and the lanes split the lights (lighting_exact_lanes); otherwise every lane with
+// `need` shades its own pixel.
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool LANES>
 __device__ __forceinline__ float4 shade_pixel_exact(const GBufferArgs& gb, const PassArgs& ps,
                                                     const float4* __restrict__ lights, const float4* __restrict__ env,
                                                     int64_t idx, bool need, bool faithful_finish) {
-    idx = need ? idx : 0;
+    if (!LANES) idx = need ? idx : 0;
     const f3 pos = mk3(gb.plane[0][idx], gb.plane[1][idx], gb.plane[2][idx]);
     const f3 n = mk3(gb.plane[3][idx], gb.plane[4][idx], gb.plane[5][idx]);
     const f3 albedo = mk3(gb.plane[6][idx], gb.plane[7][idx], gb.plane[8][idx]);
@@ -837,23 +876,34 @@ __device__ __forceinline__ float4 shade_pixel_exact(const GBufferArgs& gb, const
     const f3 eye = mk3(ps.eye[0], ps.eye[1], ps.eye[2]);
     const PixelInvariants q = make_invariants(n, normalize3(sub3(eye, pos)), albedo, f0, metallic, roughness);
     f3 d, unused;
-    lighting_exact_wave(q, q, pos, pos, need, false, lights, ps, d, unused);
+    if (LANES)
+        d = lighting_exact_lanes(q, pos, lights, ps);
+    else
+        lighting_exact_wave(q, q, pos, pos, need, false, lights, ps, d, unused);
     return finish_pixel<AMBIENT, APPLY_AO>(q, ao, d, ps, env, false, faithful_finish);
 }
 
+// A wave re-passes up to this many pixels one at a time with the lanes splitting the lights (each costs about
+// one light's IEEE sequence plus the ordered adds); more, and every lane takes its own pixels.
+constexpr int kLanesRepassMax = 8;
+
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, bool FAITHFUL>
-__global__ __launch_bounds__(kBlock, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBufferArgs gb, PassArgs ps,
+__global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBufferArgs gb, PassArgs ps,
                                                             const float4* __restrict__ lights,
                                                             const float4* __restrict__ env, FrameArgs fr,
                                                             int32_t* __restrict__ tile_kept) {
     load_libm_tables();  // powf tables -> LDS: the exact finish's gamma, spot cones, the faithful gamma's edges
     __syncthreads();
     TL_BEGIN();
+    // One wave per workgroup (blockIdx.y = 4 * tile row + wave): a wave's slot on its SIMD is refilled as soon as
+    // it ends. With 4-wave workgroups a new workgroup waited for four free slots on the CU (the wave timeline's
+    // slot refill gap, 1.0-1.7 us per wave of a ~11 us life on config 2).
     const int tid = threadIdx.x;
-    const int wave_id = __builtin_amdgcn_readfirstlane(tid) >> 6;
-    const int64_t wave_global = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
+    const int wave_id = blockIdx.y & 3;
+    const int tile_y = blockIdx.y >> 2;
+    const int64_t wave_global = ((int64_t)tile_y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
     const int xa = blockIdx.x * kTileW + 2 * (tid & 31);
-    const int y = blockIdx.y * kTileH + (tid >> 5);
+    const int y = tile_y * kTileH + 2 * wave_id + (tid >> 5);
     const bool va = (xa < gb.width) && (y < gb.height);
     const bool vb = (xa + 1 < gb.width) && (y < gb.height);
     const int geo_px = __popcll(lanes(va)) + __popcll(lanes(vb));
@@ -932,10 +982,10 @@ __global__ __launch_bounds__(kBlock, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(
             const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
             const int ln = lane_id_fresh();
             const int sx = blockIdx.x * kTileW + 2 * (ln & 31);
-            const int64_t orow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
+            const int64_t orow = (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
             float ao_a = 1.0f, ao_b = 1.0f;
             if (APPLY_AO) {
-                const int64_t arow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
+                const int64_t arow = (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
                 if (vb && gb.pairs_aligned) {
                     const float2 t = *reinterpret_cast<const float2*>(gb.plane[11] + arow);
                     ao_a = t.x;
@@ -963,20 +1013,35 @@ __global__ __launch_bounds__(kBlock, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(
         st[kStatGeometryPixels] = geo_px;
         st[kStatBackfaceTests] = 0;
     }
-    if (n_exact != 0) {  // wave-uniform, rare: the IEEE path, one pixel of the pair at a time
-        const int ln = lane_id_fresh();
-        const int rx = blockIdx.x * kTileW + 2 * (ln & 31);
-        const int ry = blockIdx.y * kTileH + 2 * wave_id + (ln >> 5);
-        const int64_t gi = (int64_t)ry * gb.row_stride + rx, oi = (int64_t)ry * fr.out_stride + rx;
-        if (lanes(need_a) != 0) {
-            const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO>(gb, ps, lights, env, gi, need_a,
-                                                                            faithful_wave);
-            if (need_a) store_pixel(fr, oi, c);
-        }
-        if (lanes(need_b) != 0) {
-            const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO>(gb, ps, lights, env, gi + 1, need_b,
-                                                                            faithful_wave);
-            if (need_b) store_pixel(fr, oi + 1, c);
+    if (n_exact != 0) {  // wave-uniform, rare: the IEEE path
+        if (n_exact <= kLanesRepassMax) {  // pixel by pixel, the lanes splitting the lights
+            uint64_t ma = lanes(need_a), mb = lanes(need_b);
+            while ((ma | mb) != 0) {
+                const bool second = ma == 0;
+                uint64_t& m = second ? mb : ma;
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                const int rx = blockIdx.x * kTileW + 2 * (l & 31) + (second ? 1 : 0);
+                const int ry = tile_y * kTileH + 2 * wave_id + (l >> 5);
+                const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, true>(
+                    gb, ps, lights, env, (int64_t)ry * gb.row_stride + rx, true, faithful_wave);
+                if (tid == 0) store_pixel(fr, (int64_t)ry * fr.out_stride + rx, c);
+            }
+        } else {  // one pixel of the pair at a time, each lane its own
+            const int ln = lane_id_fresh();
+            const int rx = blockIdx.x * kTileW + 2 * (ln & 31);
+            const int ry = tile_y * kTileH + 2 * wave_id + (ln >> 5);
+            const int64_t gi = (int64_t)ry * gb.row_stride + rx, oi = (int64_t)ry * fr.out_stride + rx;
+            if (lanes(need_a) != 0) {
+                const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi, need_a,
+                                                                                       faithful_wave);
+                if (need_a) store_pixel(fr, oi, c);
+            }
+            if (lanes(need_b) != 0) {
+                const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi + 1,
+                                                                                       need_b, faithful_wave);
+                if (need_b) store_pixel(fr, oi + 1, c);
+            }
         }
     }
     TL_FLAGS((n_exact != 0 ? 1 : 0) | (FAITHFUL && !faithful_wave ? 2 : 0));
@@ -1231,12 +1296,13 @@ static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
         dim3 grid((a.gb.width + kTileW - 1) / kTileW, (a.gb.height + kTileH - 1) / kTileH);
         if (!CULL && a.ps.balanced != 0)
             return launch_balanced<AMBIENT, F0_PLANE, APPLY_AO>(a, grid, stream);
-        if (a.lean) {  // uniform loops, no sky pass (shade_lean_kernel)
+        if (a.lean) {  // uniform loops, no sky pass (shade_lean_kernel): one wave per workgroup
+            const dim3 wgrid(grid.x, grid.y * (kBlock / 64));
             if (a.ps.faithful)
-                hipLaunchKernelGGL((shade_lean_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL, true>), grid, dim3(kBlock), 0,
+                hipLaunchKernelGGL((shade_lean_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL, true>), wgrid, dim3(64), 0,
                                    stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept);
             else
-                hipLaunchKernelGGL((shade_lean_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL, false>), grid, dim3(kBlock), 0,
+                hipLaunchKernelGGL((shade_lean_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL, false>), wgrid, dim3(64), 0,
                                    stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept);
         } else
             hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL>), grid, dim3(kBlock), 0, stream,
