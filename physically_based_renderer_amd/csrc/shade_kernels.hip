@@ -887,22 +887,16 @@ __device__ __forceinline__ float4 shade_pixel_exact(const GBufferArgs& gb, const
 // one light's IEEE sequence plus the ordered adds); more, and every lane takes its own pixels.
 constexpr int kLanesRepassMax = 8;
 
+// One wave's 64x2 pixels: wave wave_id (tile rows 2 wave_id, 2 wave_id + 1) of tile (tile_x, tile_y), statistics
+// slot wave_global. The caller has staged the powf tables.
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, bool FAITHFUL>
-__global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBufferArgs gb, PassArgs ps,
-                                                            const float4* __restrict__ lights,
-                                                            const float4* __restrict__ env, FrameArgs fr,
-                                                            int32_t* __restrict__ tile_kept) {
-    load_libm_tables();  // powf tables -> LDS: the exact finish's gamma, spot cones, the faithful gamma's edges
-    __syncthreads();
+__device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs& ps, const float4* __restrict__ lights,
+                                          const float4* __restrict__ env, const FrameArgs& fr,
+                                          int32_t* __restrict__ tile_kept, int tile_x, int tile_y, int wave_id,
+                                          int64_t wave_global) {
     TL_BEGIN();
-    // One wave per workgroup (blockIdx.y = 4 * tile row + wave): a wave's slot on its SIMD is refilled as soon as
-    // it ends. With 4-wave workgroups a new workgroup waited for four free slots on the CU (the wave timeline's
-    // slot refill gap, 1.0-1.7 us per wave of a ~11 us life on config 2).
     const int tid = threadIdx.x;
-    const int wave_id = blockIdx.y & 3;
-    const int tile_y = blockIdx.y >> 2;
-    const int64_t wave_global = ((int64_t)tile_y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
-    const int xa = blockIdx.x * kTileW + 2 * (tid & 31);
+    const int xa = tile_x * kTileW + 2 * (tid & 31);
     const int y = tile_y * kTileH + 2 * wave_id + (tid >> 5);
     const bool va = (xa < gb.width) && (y < gb.height);
     const bool vb = (xa + 1 < gb.width) && (y < gb.height);
@@ -981,7 +975,7 @@ __global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBuf
             // Finish and store every pixel the fast loop settled.
             const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
             const int ln = lane_id_fresh();
-            const int sx = blockIdx.x * kTileW + 2 * (ln & 31);
+            const int sx = tile_x * kTileW + 2 * (ln & 31);
             const int64_t orow = (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
             float ao_a = 1.0f, ao_b = 1.0f;
             if (APPLY_AO) {
@@ -1021,7 +1015,7 @@ __global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBuf
                 uint64_t& m = second ? mb : ma;
                 const int l = __builtin_ctzll(m);
                 m &= m - 1;
-                const int rx = blockIdx.x * kTileW + 2 * (l & 31) + (second ? 1 : 0);
+                const int rx = tile_x * kTileW + 2 * (l & 31) + (second ? 1 : 0);
                 const int ry = tile_y * kTileH + 2 * wave_id + (l >> 5);
                 const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, true>(
                     gb, ps, lights, env, (int64_t)ry * gb.row_stride + rx, true, faithful_wave);
@@ -1029,7 +1023,7 @@ __global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBuf
             }
         } else {  // one pixel of the pair at a time, each lane its own
             const int ln = lane_id_fresh();
-            const int rx = blockIdx.x * kTileW + 2 * (ln & 31);
+            const int rx = tile_x * kTileW + 2 * (ln & 31);
             const int ry = tile_y * kTileH + 2 * wave_id + (ln >> 5);
             const int64_t gi = (int64_t)ry * gb.row_stride + rx, oi = (int64_t)ry * fr.out_stride + rx;
             if (lanes(need_a) != 0) {
@@ -1046,6 +1040,23 @@ __global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBuf
     }
     TL_FLAGS((n_exact != 0 ? 1 : 0) | (FAITHFUL && !faithful_wave ? 2 : 0));
     TL_END(wave_global);
+}
+
+// One wave per workgroup (blockIdx.y = 4 * tile row + wave): a wave's slot on its SIMD is refilled as soon as it
+// ends (with 4-wave workgroups a new workgroup waited for four free slots on the CU). Tried and dropped: a
+// persistent grid of 3 or 4 waves per SIMD walking the waves (same-box A/B config 2 0.058 -> 0.090 ms: each wave
+// then waits for its own G-buffer loads, which the independent waves overlap).
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, bool FAITHFUL>
+__global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBufferArgs gb, PassArgs ps,
+                                                            const float4* __restrict__ lights,
+                                                            const float4* __restrict__ env, FrameArgs fr,
+                                                            int32_t* __restrict__ tile_kept) {
+    load_libm_tables();  // powf tables -> LDS: the exact finish's gamma, spot cones, the faithful gamma's edges
+    __syncthreads();
+    lean_wave<AMBIENT, F0_PLANE, APPLY_AO, CULL, FAITHFUL>(gb, ps, lights, env, fr, tile_kept, blockIdx.x,
+                                                           blockIdx.y >> 2, blockIdx.y & 3,
+                                                           ((int64_t)(blockIdx.y >> 2) * gridDim.x + blockIdx.x) *
+                                                                   (kBlock / 64) + (blockIdx.y & 3));
 }
 
 // ---- One pixel per work-item (32x8 tiles) ---------------------------------------------------------
