@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PBR_ABI_VERSION 5
+#define PBR_ABI_VERSION 6
 #define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
 
 typedef enum pbr_status {
@@ -70,7 +70,7 @@ enum pbr_pass_flags {
                                          bit-identical to the unculled pass ("exact culling") */
     PBR_FLAG_EXACT_ONLY = 1u << 3,    /* validation mode: never take the exact fast division/sqrt path
                                          ("exact fast path"); output is bit-identical, slower */
-    PBR_FLAG_FAITHFUL = 1u << 4       /* tolerance mode (ABI 4): the well-conditioned divisions of the BRDF
+    PBR_FLAG_FAITHFUL = 1u << 4,      /* tolerance mode (ABI 4): the well-conditioned divisions of the BRDF
                                          (NDF, Smith G1(N.L), specular denominator, diffuse / PI,
                                          attenuation) use the hardware reciprocal (<= 1 ulp) instead of
                                          correct rounding; the ill-conditioned GGX chain and Fresnel stay
@@ -81,6 +81,10 @@ enum pbr_pass_flags {
                                          counted per wave), non-negative strengths, ambient and env texels
                                          (checked on the host), albedo >= 0 and F0 in [0, 1] (checked per
                                          wave); elsewhere the pass stays exact. */
+    PBR_FLAG_ALPHA_TEST = 1u << 5     /* ABI 6: the ALPHA_TEST permutation (alphaTestedPS, PBRApp.cpp:750-765,
+                                         Default.hlsl:111-113): fragOpacity = the G-buffer's opacity plane;
+                                         a pixel with fragOpacity - 0.1f < 0 is discarded (its output is left
+                                         untouched), others get alpha = fragOpacity. Sky pixels are not tested. */
 };
 
 /* Per-frame constants: the shading subset of cbPass (Core.hlsl:35-61, FrameResource.h:19-44) and
@@ -112,6 +116,8 @@ typedef struct pbr_gbuffer_soa {
     int32_t width;
     int32_t height;
     int64_t row_stride;       /* elements; >= width */
+    const float* opacity;     /* ABI 6: read only with PBR_FLAG_ALPHA_TEST (the opacity map, Default.hlsl:112);
+                                 may be NULL otherwise */
 } pbr_gbuffer_soa;
 
 typedef struct pbr_context pbr_context;

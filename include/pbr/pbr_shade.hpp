@@ -168,6 +168,7 @@ class DeviceGBuffer {
         g.metallic = plane(9) + off;
         g.roughness = plane(10) + off;
         g.ao = plane(11) + off;
+        g.opacity = nullptr;  // PBR_FLAG_ALPHA_TEST: set it to an opacity plane with this row stride
         g.width = width_;
         g.height = row_end - row_begin;
         g.row_stride = row_stride_;

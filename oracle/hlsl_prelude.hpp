@@ -102,8 +102,8 @@ inline float atan2(float y, float x) { return std::atan2(y, x); }
 inline float asin(float a) { return std::asin(a); }
 inline float lerp(float x, float y, float s) { return x + s * (y - x); }
 inline float3 lerp(float3 x, float3 y, float s) { return x + s * (y - x); }
-// clip(x): discard the fragment when x < 0 (Default.hlsl:113, ALPHA_TEST permutations only). The
-// harness never builds ALPHA_TEST; the flag is kept per thread so a build that did could read it.
+// clip(x): discard the fragment when x < 0 (Default.hlsl:113, ALPHA_TEST permutations only): the harness
+// clears the flag before each pixel and leaves a discarded pixel's output untouched (ref_harness.cpp).
 inline thread_local bool g_clip_discarded = false;
 inline void clip(float x) { if (x < 0.0f) g_clip_discarded = true; }
 

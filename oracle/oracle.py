@@ -20,9 +20,13 @@ ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libpbr_ref.so")
 REFERENCE_SHADER = "/root/reference/Source/Shaders/LightingUtil.hlsl"
 
-NUM_PLANES = 15
+NUM_PLANES = 15  # the product's G-buffer planes
+C_PLANES = 16    # pbr_oracle.h ORACLE_NUM_PLANES: + the ALPHA_TEST opacity plane (ORACLE_OPACITY; callers may omit it)
 PLANE_NAMES = ("px", "py", "pz", "nx", "ny", "nz", "ar", "ag", "ab",
-               "metal", "rough", "ao", "f0r", "f0g", "f0b")
+               "metal", "rough", "ao", "f0r", "f0g", "f0b", "opacity")
+# What the output buffers hold before a pass: pixels the ALPHA_TEST permutation's clip discards keep it.
+UNTOUCHED_F32 = -1.0
+UNTOUCHED_U8 = 7
 AMBIENT_CONSTANT = 0
 AMBIENT_IBL_DIFFUSE = 1
 
@@ -39,6 +43,7 @@ class _Pass(ctypes.Structure):
         ("ambient_mode", ctypes.c_int32),
         ("use_f0_plane", ctypes.c_int32),
         ("apply_ao", ctypes.c_int32),
+        ("alpha_test", ctypes.c_int32),
     ]
 
 
@@ -55,6 +60,7 @@ class OraclePass:
     ambient_mode: int = AMBIENT_CONSTANT
     use_f0_plane: bool = False
     apply_ao: bool = False
+    alpha_test: bool = False  # ALPHA_TEST permutation (Default.hlsl:111-113): needs the opacity plane
 
     def to_c(self) -> _Pass:
         p = _Pass()
@@ -66,6 +72,7 @@ class OraclePass:
         p.ambient_mode = int(self.ambient_mode)
         p.use_f0_plane = int(bool(self.use_f0_plane))
         p.apply_ao = int(bool(self.apply_ao))
+        p.alpha_test = int(bool(self.alpha_test))
         return p
 
 
@@ -100,11 +107,12 @@ def ref_available() -> bool:
 
 def _shade(fn, planes, opass: OraclePass, lights, env, n_threads: int) -> np.ndarray:
     """planes: sequence of NUM_PLANES arrays (or None), each (H, W) float32 C-contiguous."""
-    assert len(planes) == NUM_PLANES
+    planes = list(planes) + [None] * (C_PLANES - len(planes))  # 15: no opacity plane
+    assert len(planes) == C_PLANES
     ref_plane = next(p for p in planes if p is not None)
     h, w = ref_plane.shape
     keep = []
-    ptrs = (ctypes.c_void_p * NUM_PLANES)()
+    ptrs = (ctypes.c_void_p * C_PLANES)()
     for i, p in enumerate(planes):
         if p is None:
             ptrs[i] = None
@@ -123,7 +131,7 @@ def _shade(fn, planes, opass: OraclePass, lights, env, n_threads: int) -> np.nda
         eh, ew = env_arr.shape[:2]
         keep.append(env_arr)
         env_ptr = env_arr.ctypes.data
-    out = np.empty((h, w, 4), np.float32)
+    out = np.full((h, w, 4), UNTOUCHED_F32, np.float32)
     cp = opass.to_c()
     rc = fn(w, h, w, ptrs, ctypes.byref(cp), lights_arr.ctypes.data, env_ptr, ew, eh,
             out.ctypes.data, w, int(n_threads))
@@ -197,11 +205,12 @@ def _texture(t):
 
 
 def _shade_frame(fn, planes, opass: OraclePass, lights, env, sky, coverage, fmt, n_threads):
-    assert len(planes) == NUM_PLANES
+    planes = list(planes) + [None] * (C_PLANES - len(planes))  # 15: no opacity plane
+    assert len(planes) == C_PLANES
     ref_plane = next(p for p in planes if p is not None)
     h, w = ref_plane.shape
     keep = []
-    ptrs = (ctypes.c_void_p * NUM_PLANES)()
+    ptrs = (ctypes.c_void_p * C_PLANES)()
     for i, p in enumerate(planes):
         if p is None:
             ptrs[i] = None
@@ -225,7 +234,8 @@ def _shade_frame(fn, planes, opass: OraclePass, lights, env, sky, coverage, fmt,
         keep.append(cov)
         fr.coverage, fr.coverage_stride = cov.ctypes.data, w
     fr.format = int(fmt)
-    out = np.empty((h, w, 4), np.uint8 if fmt == OUTPUT_RGBA8 else np.float32)
+    out = (np.full((h, w, 4), UNTOUCHED_U8, np.uint8) if fmt == OUTPUT_RGBA8
+           else np.full((h, w, 4), UNTOUCHED_F32, np.float32))
     cp = opass.to_c()
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p),

@@ -203,10 +203,18 @@ typedef struct {
 } job_t;
 
 /* PS, Default.hlsl:47-161, one pixel. N is the already-resolved G-buffer normal (lines 50, 104-109
- * belong to the G-buffer fill). */
-static void shade_pixel(const job_t* j, int64_t idx, float* o) {
+ * belong to the G-buffer fill). Returns 0 when the ALPHA_TEST permutation's clip discards the pixel
+ * (its output is then left as it was). */
+static int shade_pixel(const job_t* j, int64_t idx, float* o) {
     const float* const* P = j->planes;
     const oracle_pass* ps = j->pass;
+    /* fragOpacity: the opacity map under ALPHA_TEST, clip(fragOpacity - 0.1f) (discard when negative;
+     * NaN is not), else g_Opacity -- Default.hlsl:111-116 */
+    float frag_opacity = ps->opacity;
+    if (ps->alpha_test) {
+        frag_opacity = P[ORACLE_OPACITY][idx];
+        if (frag_opacity - 0.1f < 0.0f) return 0;
+    }
     v3 pos = v3make(P[ORACLE_PX][idx], P[ORACLE_PY][idx], P[ORACLE_PZ][idx]);
     v3 n = v3make(P[ORACLE_NX][idx], P[ORACLE_NY][idx], P[ORACLE_NZ][idx]);
     /* V = normalize(g_CameraPosW - pin.PosW), Default.hlsl:53 */
@@ -271,7 +279,8 @@ static void shade_pixel(const job_t* j, int64_t idx, float* o) {
     o[0] = powf(lit.x, inv_gamma);
     o[1] = powf(lit.y, inv_gamma);
     o[2] = powf(lit.z, inv_gamma);
-    o[3] = ps->opacity; /* Default.hlsl:160 */
+    o[3] = frag_opacity; /* Default.hlsl:160 */
+    return 1;
 }
 
 /* The sky pass for a background pixel, Skybox.hlsl:37-49: sampleCoord = normalize(PosW) (the sky
@@ -309,8 +318,8 @@ static void* run_rows(void* arg) {
             float px[4];
             if (j->coverage && j->coverage[(int64_t)y * j->coverage_stride + x] == 0)
                 sky_pixel(j, idx, px);
-            else
-                shade_pixel(j, idx, px);
+            else if (!shade_pixel(j, idx, px))
+                continue; /* clip: the render target keeps its value */
             if (j->format == ORACLE_OUTPUT_RGBA8) {
                 uint8_t* o8 = (uint8_t*)j->out_any + off * 4;
                 for (int c = 0; c < 4; ++c) o8[c] = oracle_unorm8(px[c]);
@@ -343,6 +352,7 @@ int oracle_shade_frame(int width, int height, int64_t stride, const float* const
         if (!planes[p]) return -1;
     if (pass->apply_ao && !planes[ORACLE_AO]) return -1;
     if (pass->use_f0_plane && (!planes[ORACLE_F0R] || !planes[ORACLE_F0G] || !planes[ORACLE_F0B])) return -1;
+    if (pass->alpha_test && !planes[ORACLE_OPACITY]) return -1;
     if (width == 0 || height == 0) return 0;
     if (n_threads < 1) n_threads = 1;
     if (n_threads > height) n_threads = height;

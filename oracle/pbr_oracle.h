@@ -42,6 +42,7 @@ enum {
     ORACLE_AR, ORACLE_AG, ORACLE_AB,
     ORACLE_METAL, ORACLE_ROUGH, ORACLE_AO,
     ORACLE_F0R, ORACLE_F0G, ORACLE_F0B,
+    ORACLE_OPACITY,        /* the ALPHA_TEST permutation's opacity map (Default.hlsl:111-112) */
     ORACLE_NUM_PLANES
 };
 
@@ -54,6 +55,8 @@ typedef struct oracle_pass {
     int32_t ambient_mode;  /* ORACLE_AMBIENT_*  */
     int32_t use_f0_plane;  /* SPECULAR_TEXTURE permutation  Default.hlsl:91-96 */
     int32_t apply_ao;      /* extension: ambient *= AO (reference: off) */
+    int32_t alpha_test;    /* ALPHA_TEST permutation (PBRApp.cpp:750-765): fragOpacity = the opacity plane,
+                              clip(fragOpacity - 0.1f) leaves the pixel's output untouched  Default.hlsl:111-113 */
 } oracle_pass;
 
 /*

@@ -17,7 +17,9 @@
 // Permutations (the D3D_SHADER_MACRO defines of PBRApp.cpp:715-754): DIFFUSE/METALLIC/ROUGHNESS/NORMAL
 // _TEXTURE = 1 with the G-buffer bound as the maps (ps_binding.inc explains the exact embedding),
 // SPECULAR_TEXTURE = 1 for the F0 plane (config 4) else 0 (F0 = lerp(g_FresnelR0, albedo, metallic)),
-// ALPHA_TEST = 0. The light counts NUM_DIR/POINT/SPOT_LIGHTS (Core.hlsl:1-12) are compile-time in the
+// ALPHA_TEST = 0, and the ALPHA_TEST = 1 permutation of the same four (the reference's alphaTestedPS,
+// PBRApp.cpp:750-765: the opacity map bound as the G-buffer's opacity plane; clip() in hlsl_prelude.hpp marks
+// the pixel discarded and the harness leaves its output untouched). The light counts NUM_DIR/POINT/SPOT_LIGHTS (Core.hlsl:1-12) are compile-time in the
 // reference; here they are runtime values behind macros whose preprocessor value is 1, so the
 // `#if (NUM_*_LIGHTS > 0)` guards of ComputeLighting (LightingUtil.hlsl:178, 185, 192) keep their loops
 // and each loop runs the pass's count (a loop with zero trips is what the #if removes). The shipped
@@ -123,6 +125,30 @@ namespace ps_ibl_f0map {
 #include "ps_binding.inc"
 }  // namespace ps_ibl_f0map
 #undef SPECULAR_TEXTURE
+#undef ALPHA_TEST
+#define ALPHA_TEST 1
+#define SPECULAR_TEXTURE 0
+namespace ps_const_at {
+#include "Default.hlsl"
+#include "ps_binding.inc"
+}  // namespace ps_const_at
+namespace ps_ibl_at {
+#include "Default_ibl.hlsl"
+#include "ps_binding.inc"
+}  // namespace ps_ibl_at
+#undef SPECULAR_TEXTURE
+#define SPECULAR_TEXTURE 1
+namespace ps_const_f0map_at {
+#include "Default.hlsl"
+#include "ps_binding.inc"
+}  // namespace ps_const_f0map_at
+namespace ps_ibl_f0map_at {
+#include "Default_ibl.hlsl"
+#include "ps_binding.inc"
+}  // namespace ps_ibl_f0map_at
+#undef SPECULAR_TEXTURE
+#undef ALPHA_TEST
+#define ALPHA_TEST 0
 #undef NUM_DIR_LIGHTS
 #undef NUM_POINT_LIGHTS
 #undef NUM_SPOT_LIGHTS
@@ -153,10 +179,11 @@ using namespace hlsl;
 
 namespace {
 
-enum Variant { kShipped, kConst, kIbl, kConstF0, kIblF0 };
+enum Variant { kShipped, kConst, kIbl, kConstF0, kIblF0, kConstAt, kIblAt, kConstF0At, kIblF0At };
 
 Variant pick(const oracle_pass& ps) {
     const bool ibl = ps.ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE;
+    if (ps.alpha_test) return ps.use_f0_plane ? (ibl ? kIblF0At : kConstF0At) : (ibl ? kIblAt : kConstAt);
     if (ps.use_f0_plane) return ibl ? kIblF0 : kConstF0;
     if (ibl) return kIbl;
     if (ps.n_dir == ps_shipped::kDir && ps.n_point == ps_shipped::kPoint && ps.n_spot == ps_shipped::kSpot)
@@ -174,6 +201,10 @@ void bind(Variant v, const oracle_pass& ps, const oracle_light* lights, const Te
         case kIbl: ps_ibl::pbr_bind_pass(ps, lights, env); break;
         case kConstF0: ps_const_f0map::pbr_bind_pass(ps, lights, env); break;
         case kIblF0: ps_ibl_f0map::pbr_bind_pass(ps, lights, env); break;
+        case kConstAt: ps_const_at::pbr_bind_pass(ps, lights, env); break;
+        case kIblAt: ps_ibl_at::pbr_bind_pass(ps, lights, env); break;
+        case kConstF0At: ps_const_f0map_at::pbr_bind_pass(ps, lights, env); break;
+        case kIblF0At: ps_ibl_f0map_at::pbr_bind_pass(ps, lights, env); break;
     }
     if (ps.apply_ao && v != kConst) ps_const::pbr_bind_pass(ps, lights, env);  // ps_pixel_ao_extension's
 }
@@ -196,7 +227,12 @@ float4 ps_pixel_ao_extension(const float* const* planes, int64_t i, const oracle
         F0 = float3(ps.fresnel_r0[0], ps.fresnel_r0[1], ps.fresnel_r0[2]);                  // :94
         F0 = lerp(F0, diffuseAlbedo, metallic);                                             // :95
     }
-    ps_const::Material mat = {diffuseAlbedo, metallic, F0, roughness, float3(1.0f), ps.opacity,
+    float fragOpacity = ps.opacity;                                                        // :115
+    if (ps.alpha_test) {                                                                    // :111-113
+        fragOpacity = planes[ORACLE_OPACITY][i];
+        clip(fragOpacity - 0.1f);
+    }
+    ps_const::Material mat = {diffuseAlbedo, metallic, F0, roughness, float3(1.0f), fragOpacity,
                               float3(0.0f), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};                  // :121-133
     float3 shadowFactor = 1.0f;
     float3 directLight = ps_const::ComputeLighting(ps_const::cbPass::g_Lights, mat, PosW, N, V, shadowFactor);
@@ -215,7 +251,7 @@ float4 ps_pixel_ao_extension(const float* const* planes, int64_t i, const oracle
     float3 litColor = ambient + directLight;
     litColor = litColor / (litColor + float3(1.0f, 1.0f, 1.0f));  // :153
     litColor = pow(litColor, (1.0f / 2.2f));                      // :155
-    return float4(litColor, ps.opacity);                          // :160
+    return float4(litColor, fragOpacity);                         // :160
 }
 
 float4 shade_pixel(Variant v, const float* const* planes, int64_t i, const oracle_pass& ps, const Texture2D& env) {
@@ -226,6 +262,10 @@ float4 shade_pixel(Variant v, const float* const* planes, int64_t i, const oracl
         case kIbl: return ps_ibl::pbr_shade_pixel(planes, i);
         case kConstF0: return ps_const_f0map::pbr_shade_pixel(planes, i);
         case kIblF0: return ps_ibl_f0map::pbr_shade_pixel(planes, i);
+        case kConstAt: return ps_const_at::pbr_shade_pixel(planes, i);
+        case kIblAt: return ps_ibl_at::pbr_shade_pixel(planes, i);
+        case kConstF0At: return ps_const_f0map_at::pbr_shade_pixel(planes, i);
+        case kIblF0At: return ps_ibl_f0map_at::pbr_shade_pixel(planes, i);
     }
     return float4();
 }
@@ -249,13 +289,15 @@ bool counts_ok(const oracle_pass& ps) {
     return ps.n_dir >= 0 && ps.n_point >= 0 && ps.n_spot >= 0 &&
            (int64_t)ps.n_dir + ps.n_point + ps.n_spot <= PBR_ORACLE_MAX_LIGHTS;
 }
+bool planes_ok(const float* const* planes, const oracle_pass& ps) { return !ps.alpha_test || planes[ORACLE_OPACITY]; }
 
 }  // namespace
 
 extern "C" int ref_shade_frame(int width, int height, int64_t stride, const float* const* planes,
                                const oracle_pass* pass, const oracle_light* lights, const oracle_frame* frame,
                                void* out, int64_t out_stride, int /*n_threads*/) {
-    if (!planes || !pass || !frame || !out || width < 0 || height < 0 || !counts_ok(*pass)) return -1;
+    if (!planes || !pass || !frame || !out || width < 0 || height < 0 || !counts_ok(*pass) || !planes_ok(planes, *pass))
+        return -1;
     if (pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE && !frame->env_rgba) return -1;
     if (frame->coverage && !frame->sky_rgba) return -1;
     Texture2D env, skytex;
@@ -268,7 +310,9 @@ extern "C" int ref_shade_frame(int width, int height, int64_t stride, const floa
         for (int x = 0; x < width; ++x) {
             const int64_t i = (int64_t)y * stride + x;
             const bool background = frame->coverage && frame->coverage[(int64_t)y * frame->coverage_stride + x] == 0;
+            g_clip_discarded = false;
             const float4 c = background ? sky_pixel(planes, i) : shade_pixel(v, planes, i, *pass, env);
+            if (g_clip_discarded) continue;  // clip(): the render target keeps its value
             const int64_t off = ((int64_t)y * out_stride + x) * 4;
             if (frame->format == ORACLE_OUTPUT_RGBA8) {
                 uint8_t* o = static_cast<uint8_t*>(out) + off;
@@ -285,7 +329,7 @@ extern "C" int ref_shade_frame(int width, int height, int64_t stride, const floa
 extern "C" int ref_shade(int width, int height, int64_t stride, const float* const* planes, const oracle_pass* pass,
                          const oracle_light* lights, const uint16_t* env_rgba16, int env_w, int env_h, float* out,
                          int64_t out_stride, int /*n_threads*/) {
-    if (!planes || !pass || !out || width < 0 || height < 0 || !counts_ok(*pass)) return -1;
+    if (!planes || !pass || !out || width < 0 || height < 0 || !counts_ok(*pass) || !planes_ok(planes, *pass)) return -1;
     if (pass->ambient_mode == ORACLE_AMBIENT_IBL_DIFFUSE && !env_rgba16) return -1;
     Texture2D env;
     env.texels = env_rgba16, env.w = env_w, env.h = env_h;
@@ -293,7 +337,9 @@ extern "C" int ref_shade(int width, int height, int64_t stride, const float* con
     bind(v, *pass, lights, env);
     for (int y = 0; y < height; ++y) {
         for (int x = 0; x < width; ++x) {
+            g_clip_discarded = false;
             const float4 c = shade_pixel(v, planes, (int64_t)y * stride + x, *pass, env);
+            if (g_clip_discarded) continue;  // clip(): the render target keeps its value
             float* o = out + ((int64_t)y * out_stride + x) * 4;
             o[0] = c.x; o[1] = c.y; o[2] = c.z; o[3] = c.w;
         }

@@ -24,6 +24,7 @@ PBR_FLAG_APPLY_AO = 1 << 1
 PBR_FLAG_TILED_CULLING = 1 << 2
 PBR_FLAG_EXACT_ONLY = 1 << 3
 PBR_FLAG_FAITHFUL = 1 << 4  # tolerance mode (pbr_shade.h): within 1e-5, not bit-identical
+PBR_FLAG_ALPHA_TEST = 1 << 5  # ALPHA_TEST permutation (Default.hlsl:111-113): clip on the opacity plane
 PBR_OUTPUT_RGBA32F = 0
 PBR_OUTPUT_RGBA8_UNORM = 1
 PBR_SCENE_SPHERE_RUSTEDIRON = 1
@@ -84,6 +85,7 @@ class GBufferSoA(ctypes.Structure):
         ("width", ctypes.c_int32),
         ("height", ctypes.c_int32),
         ("row_stride", ctypes.c_int64),
+        ("opacity", ctypes.c_void_p),  # ABI 6: PBR_FLAG_ALPHA_TEST's opacity plane
     ]
 
 

@@ -283,7 +283,8 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
     if (n > 0 && !pass->lights) return PBR_ERR_INVALID_ARGUMENT;
     if (!is_ambient_mode(pass->ambient_mode)) return PBR_ERR_INVALID_ARGUMENT;
     const uint32_t known =
-        PBR_FLAG_F0_PLANE | PBR_FLAG_APPLY_AO | PBR_FLAG_TILED_CULLING | PBR_FLAG_EXACT_ONLY | PBR_FLAG_FAITHFUL;
+        PBR_FLAG_F0_PLANE | PBR_FLAG_APPLY_AO | PBR_FLAG_TILED_CULLING | PBR_FLAG_EXACT_ONLY | PBR_FLAG_FAITHFUL |
+        PBR_FLAG_ALPHA_TEST;
     if (pass->flags & ~known) return PBR_ERR_INVALID_ARGUMENT;
 
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -466,6 +467,8 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     if (!gb->metallic || !gb->roughness) return PBR_ERR_INVALID_ARGUMENT;
     if (apply_ao && !gb->ao) return PBR_ERR_INVALID_ARGUMENT;
     if (f0_plane && (!gb->f0[0] || !gb->f0[1] || !gb->f0[2])) return PBR_ERR_INVALID_ARGUMENT;
+    const bool alpha_test = (ctx->flags & PBR_FLAG_ALPHA_TEST) != 0;
+    if (alpha_test && !gb->opacity) return PBR_ERR_INVALID_ARGUMENT;
     if (ctx->ambient_mode == PBR_AMBIENT_IBL_DIFFUSE && !ctx->env.d) return PBR_ERR_NOT_READY;
     if (fr->coverage && !ctx->sky.d) return PBR_ERR_NOT_READY;  // background pixels need the sky map
 
@@ -474,11 +477,13 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
                                gb->normal_w[2], gb->albedo[0], gb->albedo[1], gb->albedo[2], gb->metallic,
                                gb->roughness, gb->ao, gb->f0[0], gb->f0[1], gb->f0[2]};
     for (int i = 0; i < 15; ++i) a.gb.plane[i] = planes[i] ? planes[i] : planes[0];
+    a.gb.plane[15] = alpha_test ? gb->opacity : planes[0];
+    a.gb.alpha_test = alpha_test;
     a.gb.width = gb->width;
     a.gb.height = gb->height;
     a.gb.row_stride = gb->row_stride;
     a.gb.pairs_aligned = (gb->row_stride % 2) == 0;
-    for (int i = 0; i < 15; ++i)
+    for (int i = 0; i < 16; ++i)
         if (!aligned(a.gb.plane[i], 8)) a.gb.pairs_aligned = false;
     a.ps = ctx->pass;
     a.ps.env_w = ctx->env.w;

@@ -10,12 +10,14 @@ constexpr int kAmbientConstant = 0;
 constexpr int kAmbientIblDiffuse = 1;
 
 // The 15 SoA planes in pbr_gbuffer_soa order: pos xyz, normal xyz, albedo rgb, metallic,
-// roughness, ao, f0 rgb. Unused planes may alias plane 0 (they are never read).
+// roughness, ao, f0 rgb, then [15] the opacity plane (PBR_FLAG_ALPHA_TEST). Unused planes may alias plane 0
+// (they are never read).
 struct GBufferArgs {
-    const float* plane[15];
+    const float* plane[16];
     int width, height;
     int64_t row_stride;
     bool pairs_aligned;  // every read plane 8-byte aligned and row_stride even: 8-byte pair loads
+    bool alpha_test;     // PBR_FLAG_ALPHA_TEST: clip on plane[15] (Default.hlsl:111-113)
 };
 
 // Pass constants passed by value as kernel arguments (the shading subset of cbPass / cbMaterial).

@@ -535,6 +535,18 @@ __device__ __forceinline__ void store_pixel(const FrameArgs& fr, int64_t off, fl
     }
 }
 
+// PBR_FLAG_ALPHA_TEST, the reference's ALPHA_TEST permutation (Default.hlsl:111-113, alphaTestedPS): fragOpacity is
+// the pixel's opacity-map value (G-buffer plane 15, index gidx) and clip(fragOpacity - 0.1f) discards the fragment
+// when that is negative (NaN is not) -- the pixel's output is then left untouched; otherwise fragOpacity is the
+// output alpha (Default.hlsl:160). Geometry pixels only (the sky PS has no clip). Returns whether to store.
+__device__ __forceinline__ bool alpha_keep(const GBufferArgs& gb, int64_t gidx, float4& c) {
+    if (!gb.alpha_test) return true;  // uniform
+    const float op = gb.plane[15][gidx];
+    if (op - 0.1f < 0.0f) return false;
+    c.w = op;
+    return true;
+}
+
 // Coverage of a pixel: geometry unless the frame has a coverage plane holding 0 there.
 __device__ __forceinline__ bool is_geometry(const FrameArgs& fr, int x, int y) {
     return fr.coverage == nullptr || fr.coverage[(int64_t)y * fr.coverage_stride + x] != 0;
@@ -796,12 +808,17 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             if (vb) ao_b = gb.plane[11][arow + 1];
         }
     }
-    if (va)
-        store_pixel(fr, orow, ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
-                                 : sky_pixel(ua.n, ps, fr.sky, !exact_only));
-    if (vb)
-        store_pixel(fr, orow + 1, gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
-                                      : sky_pixel(ub.n, ps, fr.sky, !exact_only));
+    const int64_t grow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
+    if (va) {
+        float4 c = ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
+                      : sky_pixel(ua.n, ps, fr.sky, !exact_only);
+        if (!ga || alpha_keep(gb, grow, c)) store_pixel(fr, orow, c);
+    }
+    if (vb) {
+        float4 c = gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
+                       : sky_pixel(ub.n, ps, fr.sky, !exact_only);
+        if (!gb_ || alpha_keep(gb, grow + 1, c)) store_pixel(fr, orow + 1, c);
+    }
     TL_END(((long long)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id);
 }
 
@@ -989,10 +1006,15 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
                     if (vb) ao_b = gb.plane[11][arow + 1];
                 }
             }
-            if (va && !need_a)
-                store_pixel(fr, orow, finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, lane(d2, 0), ps, env, ok_a, faithful_wave));
-            if (vb && !need_b)
-                store_pixel(fr, orow + 1, finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, lane(d2, 1), ps, env, ok_b, faithful_wave));
+            const int64_t grow = (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
+            if (va && !need_a) {
+                float4 c = finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, lane(d2, 0), ps, env, ok_a, faithful_wave);
+                if (alpha_keep(gb, grow, c)) store_pixel(fr, orow, c);
+            }
+            if (vb && !need_b) {
+                float4 c = finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, lane(d2, 1), ps, env, ok_b, faithful_wave);
+                if (alpha_keep(gb, grow + 1, c)) store_pixel(fr, orow + 1, c);
+            }
         }
     }
     const int n_exact = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
@@ -1017,9 +1039,10 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
                 m &= m - 1;
                 const int rx = tile_x * kTileW + 2 * (l & 31) + (second ? 1 : 0);
                 const int ry = tile_y * kTileH + 2 * wave_id + (l >> 5);
-                const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, true>(
+                float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, true>(
                     gb, ps, lights, env, (int64_t)ry * gb.row_stride + rx, true, faithful_wave);
-                if (tid == 0) store_pixel(fr, (int64_t)ry * fr.out_stride + rx, c);
+                if (tid == 0 && alpha_keep(gb, (int64_t)ry * gb.row_stride + rx, c))
+                    store_pixel(fr, (int64_t)ry * fr.out_stride + rx, c);
             }
         } else {  // one pixel of the pair at a time, each lane its own
             const int ln = lane_id_fresh();
@@ -1027,14 +1050,14 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
             const int ry = tile_y * kTileH + 2 * wave_id + (ln >> 5);
             const int64_t gi = (int64_t)ry * gb.row_stride + rx, oi = (int64_t)ry * fr.out_stride + rx;
             if (lanes(need_a) != 0) {
-                const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi, need_a,
-                                                                                       faithful_wave);
-                if (need_a) store_pixel(fr, oi, c);
+                float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi, need_a,
+                                                                                 faithful_wave);
+                if (need_a && alpha_keep(gb, gi, c)) store_pixel(fr, oi, c);
             }
             if (lanes(need_b) != 0) {
-                const float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi + 1,
-                                                                                       need_b, faithful_wave);
-                if (need_b) store_pixel(fr, oi + 1, c);
+                float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi + 1,
+                                                                                 need_b, faithful_wave);
+                if (need_b && alpha_keep(gb, gi + 1, c)) store_pixel(fr, oi + 1, c);
             }
         }
     }
@@ -1194,10 +1217,11 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
         st[kStatGeometryPixels] = geo_px;
         st[kStatBackfaceTests] = 0;
     }
-    if (valid)
-        store_pixel(fr, (int64_t)y * fr.out_stride + x,
-                    geom ? finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env, q.fast_ok)
-                         : sky_pixel(q.n, ps, fr.sky, !exact_only));
+    if (valid) {
+        float4 c = geom ? finish_pixel<AMBIENT, APPLY_AO>(q, ao, direct, ps, env, q.fast_ok)
+                        : sky_pixel(q.n, ps, fr.sky, !exact_only);
+        if (!geom || alpha_keep(gb, idx, c)) store_pixel(fr, (int64_t)y * fr.out_stride + x, c);
+    }
 }
 
 // The balanced-list kernels (BAL 1, 2) are compiled in their own translation unit, shade_kernels_bal.hip,

@@ -112,26 +112,34 @@ class PassConstants:
 
 class GBuffer:
     """Structure-of-arrays G-buffer: one (15, H, row_stride) fp32 tensor, plane order
-    pos xyz, normal xyz, albedo rgb, metallic, roughness, ao, f0 rgb (pbr_gbuffer_soa)."""
+    pos xyz, normal xyz, albedo rgb, metallic, roughness, ao, f0 rgb (pbr_gbuffer_soa), and, for the
+    ALPHA_TEST permutation (PBR_FLAG_ALPHA_TEST), an (H, row_stride) opacity plane with the same row stride."""
 
-    def __init__(self, planes: torch.Tensor, width: Optional[int] = None):
+    def __init__(self, planes: torch.Tensor, width: Optional[int] = None, opacity: Optional[torch.Tensor] = None):
         if planes.dim() != 3 or planes.shape[0] != N.NUM_PLANES or planes.dtype != torch.float32:
             raise ValueError("planes must be a (15, H, W) float32 tensor")
         if planes.stride(2) != 1:
             raise ValueError("planes rows must be contiguous")
+        if opacity is not None and (opacity.dim() != 2 or opacity.dtype != torch.float32 or
+                                    opacity.shape[0] != planes.shape[1] or opacity.shape[1] < planes.shape[2] or
+                                    opacity.stride(1) != 1 or opacity.stride(0) != planes.stride(1) or
+                                    opacity.device != planes.device):
+            raise ValueError("opacity must be an (H, W) float32 plane with the planes' row stride and device")
         self.planes = planes
+        self.opacity = opacity
         self.height = planes.shape[1]
         self.width = planes.shape[2] if width is None else width
         self.row_stride = planes.stride(1)
 
     @classmethod
-    def from_host(cls, planes: np.ndarray, device) -> "GBuffer":
+    def from_host(cls, planes: np.ndarray, device, opacity: Optional[np.ndarray] = None) -> "GBuffer":
         t = torch.from_numpy(np.ascontiguousarray(planes, dtype=np.float32))
-        return cls(t.to(device))
+        o = None if opacity is None else torch.from_numpy(np.ascontiguousarray(opacity, dtype=np.float32)).to(device)
+        return cls(t.to(device), opacity=o)
 
     def rows(self, r0: int, r1: int) -> "GBuffer":
         """A row band (a view: shading it writes only those rows)."""
-        return GBuffer(self.planes[:, r0:r1, :], self.width)
+        return GBuffer(self.planes[:, r0:r1, :], self.width, None if self.opacity is None else self.opacity[r0:r1])
 
     def to_c(self) -> N.GBufferSoA:
         g = N.GBufferSoA()
@@ -144,6 +152,7 @@ class GBuffer:
         g.metallic, g.roughness, g.ao = ptr[9], ptr[10], ptr[11]
         g.f0[:] = ptr[12:15]
         g.width, g.height, g.row_stride = int(self.width), int(self.height), int(self.row_stride)
+        g.opacity = None if self.opacity is None else self.opacity.data_ptr()
         return g
 
 
@@ -222,7 +231,7 @@ class ShadingContext:
 
     def shade(self, gb: GBuffer, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
         """Shade every pixel of ``gb`` into ``out`` ((H, >=W, 4) fp32 on the device), asynchronously."""
-        self._check_device(gb.planes, out)
+        self._check_device(gb.planes, gb.opacity, out)
         if out is None:
             out = torch.empty((gb.height, gb.width, 4), dtype=torch.float32, device=gb.planes.device)
         if out.dtype != torch.float32 or out.dim() != 3 or out.shape[2] != 4 or out.stride(2) != 1 or out.stride(1) != 4:
@@ -239,7 +248,7 @@ class ShadingContext:
                     fmt: int = N.PBR_OUTPUT_RGBA32F, stream=None) -> torch.Tensor:
         """Shade ``gb`` with the sky pass on background pixels (``coverage`` == 0; (H, >=W) uint8 on the
         device) into ``out``: (H, W, 4) float32 for RGBA32F or (H, W, 4) uint8 for RGBA8_UNORM."""
-        self._check_device(gb.planes, out, coverage)
+        self._check_device(gb.planes, gb.opacity, out, coverage)
         dev = gb.planes.device
         if fmt == N.PBR_OUTPUT_RGBA8_UNORM:
             dtype, px_bytes = torch.uint8, 4

@@ -34,8 +34,23 @@ _ensure_built()
 
 
 def golden_names():
-    """Fixtures of the PS path (oracle_shade / pbr_shade_gbuffer)."""
-    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz") and not f.startswith("frame_"))
+    """Fixtures of the PS path (oracle_shade / pbr_shade_gbuffer), ALPHA_TEST fixtures excluded."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR)
+                  if f.endswith(".npz") and not f.startswith(("frame_", "alpha_test_")))
+
+
+def alpha_golden_names():
+    """Fixtures of the ALPHA_TEST permutation (Default.hlsl:111-113): planes + opacity plane."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz") and f.startswith("alpha_test_"))
+
+
+def load_alpha_golden(name, env_png=None):
+    """dict(planes (15,H,W), opacity (H,W), lights, meta, expected, coverage or None, sky (uint16) or None, env)."""
+    z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"))  # numeric arrays only: allow_pickle stays False
+    meta = json.loads(str(z["meta"]))
+    return dict(planes=z["planes"], opacity=z["opacity"], lights=z["lights"], meta=meta, expected=z["expected"],
+                coverage=z["coverage"] if "coverage" in z.files else None,
+                sky=z["sky_u16"] if "sky_u16" in z.files else None, env=env_png if meta["env"] else None)
 
 
 def frame_golden_names():
@@ -70,7 +85,8 @@ def oracle_pass_from_meta(meta):
     return O.OraclePass(eye=tuple(meta["eye"]), ambient=tuple(meta["ambient"]),
                         fresnel_r0=tuple(meta["fresnel_r0"]), opacity=meta["opacity"], n_dir=meta["n_dir"],
                         n_point=meta["n_point"], n_spot=meta["n_spot"], ambient_mode=meta["ambient_mode"],
-                        use_f0_plane=meta["use_f0_plane"], apply_ao=meta["apply_ao"])
+                        use_f0_plane=meta["use_f0_plane"], apply_ao=meta["apply_ao"],
+                        alpha_test=meta.get("alpha_test", False))
 
 
 def oracle_pass_from_constants(pc):
@@ -80,7 +96,8 @@ def oracle_pass_from_constants(pc):
     return O.OraclePass(eye=tuple(pc.eye_pos_w), ambient=tuple(pc.ambient_light), fresnel_r0=tuple(pc.fresnel_r0),
                         opacity=pc.opacity, n_dir=pc.num_dir_lights, n_point=pc.num_point_lights,
                         n_spot=pc.num_spot_lights, ambient_mode=pc.ambient_mode,
-                        use_f0_plane=bool(pc.flags & 1), apply_ao=bool(pc.flags & 2))
+                        use_f0_plane=bool(pc.flags & 1), apply_ao=bool(pc.flags & 2),
+                        alpha_test=bool(pc.flags & 32))
 
 
 @pytest.fixture(scope="session")

@@ -10,6 +10,7 @@ reproduces every one of them bit for bit (tests/test_oracle_golden.py::test_refe
 
     make -C oracle all ref && python tests/golden/gen_golden.py            # everything
     python tests/golden/gen_golden.py --frames                              # frame_*.npz only
+    python tests/golden/gen_golden.py --alpha                               # alpha_test_*.npz only
 
 The frame_* fixtures cover pbr_shade_frame: a coverage plane with background pixels (the sky pass of
 Skybox.hlsl:37-49 on a procedural sky texture), R8G8B8A8_UNORM output, and an fp32 HDR environment.
@@ -330,11 +331,68 @@ def make_frames():
         print(f"{name:32s} {planes.shape[1] * planes.shape[2]:6d} px  background={int((cov == 0).sum())}")
 
 
+def alpha_planes(rng, h):
+    """A G-buffer for the ALPHA_TEST permutation and its opacity plane: values either side of the 0.1 cut
+    (0.1 itself, the floats next to it, 0, -0, NaN, +-inf, > 1) and uniform ones."""
+    p = empty_planes(h, W)[:15]
+    p[0:3] = random_points(rng, h, W, (-10, -10, 0), (10, 10, 10))
+    p[3:6] = unit(rng.uniform(-1, 1, (3, h, W))).astype(np.float32)
+    p[6:11] = rng.uniform(0, 1, (5, h, W)).astype(np.float32)
+    p[12:15] = rng.uniform(0, 1, (3, h, W)).astype(np.float32)
+    op = rng.uniform(0.0, 0.3, (h, W)).astype(np.float32)
+    cut = np.float32(0.1)
+    special = [cut, np.nextafter(cut, np.float32(0)), np.nextafter(cut, np.float32(1)), 0.0, -0.0, np.nan, 1.5,
+               np.float32(0.1000001), np.float32(0.0999999), np.inf, -np.inf]
+    op[0, :len(special)] = np.asarray(special, np.float32)
+    return p.astype(np.float32), op
+
+
+ALPHA_CASES = {  # name -> (ambient, F0 plane, coverage)
+    "alpha_test_const": (O.AMBIENT_CONSTANT, False, False),
+    "alpha_test_ibl_f0plane": (O.AMBIENT_IBL_DIFFUSE, True, False),
+    "alpha_test_frame_sky": (O.AMBIENT_CONSTANT, False, True),
+}
+
+
+def make_alpha():
+    """The ALPHA_TEST permutation (alphaTestedPS, Default.hlsl:111-113) through the reference build: discarded
+    pixels keep the output buffer's prior contents (oracle.UNTOUCHED_F32)."""
+    env_png = envmap.load_chelsea_stairs_env()
+    sky = envmap.procedural_sky_rgba16(96, 48)
+    for k, (name, (amb, f0, frame)) in enumerate(ALPHA_CASES.items()):
+        rng = np.random.default_rng(3000 + k)
+        planes, op = alpha_planes(rng, 16)
+        lights = np.asarray(REF_DIR_LIGHTS + rand_lights(rng, 8, "point") + rand_lights(rng, 2, "spot"),
+                            np.float32).reshape(-1, 12)
+        ps = O.OraclePass(n_dir=4, n_point=8, n_spot=2, ambient_mode=amb, use_f0_plane=f0, alpha_test=True,
+                          opacity=0.75)
+        env = env_png if amb == O.AMBIENT_IBL_DIFFUSE else None
+        extra = {}
+        if frame:
+            cov = (rng.uniform(size=planes.shape[1:]) >= 0.3).astype(np.uint8)
+            expected = O.shade_frame_ref(list(planes) + [op], ps, lights, env, sky, cov, O.OUTPUT_RGBA32F)
+            extra = dict(coverage=cov, sky_u16=sky)
+        else:
+            expected = O.shade_ref(list(planes) + [op], ps, lights, env)
+        meta = dict(eye=list(ps.eye), ambient=list(ps.ambient), fresnel_r0=list(ps.fresnel_r0),
+                    opacity=ps.opacity, n_dir=ps.n_dir, n_point=ps.n_point, n_spot=ps.n_spot,
+                    ambient_mode=ps.ambient_mode, use_f0_plane=bool(ps.use_f0_plane), apply_ao=False,
+                    alpha_test=True, env="Chelsea_Stairs_Env.png" if env is not None else "",
+                    untouched=O.UNTOUCHED_F32)
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), planes=planes, opacity=op, lights=lights,
+                            expected=expected, meta=np.array(json.dumps(meta)), **extra)
+        kept = (expected[..., 3] != O.UNTOUCHED_F32).sum()
+        print(f"{name:32s} {planes.shape[1] * planes.shape[2]:6d} px  shaded={int(kept)}")
+
+
 def main():
     if not O.ref_available():
         sys.exit("oracle/_ref/libpbr_ref.so missing: make -C oracle ref (needs /root/reference)")
     if "--frames" in sys.argv:
         make_frames()
+        return
+    if "--alpha" in sys.argv:
+        make_alpha()
         return
         sys.exit("oracle/_ref/libpbr_ref.so missing: make -C oracle ref (needs /root/reference)")
     env = envmap.load_chelsea_stairs_env()
@@ -354,6 +412,7 @@ def main():
         print(f"{name:32s} {planes.shape[1] * planes.shape[2]:6d} px  lights={lights.shape[0]:3d}  "
               f"nan={int(np.isnan(expected).any(axis=-1).sum())}")
     make_frames()
+    make_alpha()
 
 
 if __name__ == "__main__":

@@ -5,6 +5,8 @@ that bench.py reads for roofline.traffic.
 HBM bytes per launch = FETCH_SIZE x 2 + WRITE_SIZE (KiB; gfx950 FETCH_SIZE reports half of a
 coalesced read, MI355X_MICROARCH.md "HBM"), averaged over the shading kernel's dispatches.
 usage: python tools/pmc_summarize.py <tag> <workload> <pixels> <bytes_per_px> <lights> <revision> [<profiles subdir>]
+The kernel_sources_sha stamp is computed from this checkout, or, with PBR_PROFILED_TREE=<dir>, from a checkout of
+the profiled revision (a git worktree) when the sources have moved on since the run.
 """
 import csv
 import glob
@@ -19,6 +21,19 @@ sys.path.insert(0, ROOT)
 from physically_based_renderer_amd._native import kernel_sources_sha  # noqa: E402
 
 
+def profiled_sources_sha():
+    tree = os.environ.get("PBR_PROFILED_TREE")
+    if not tree:
+        return kernel_sources_sha()
+    import physically_based_renderer_amd._native as nat
+    saved = nat.HEADER_PATH
+    nat.HEADER_PATH = os.path.join(tree, "include", "pbr", "pbr_shade.h")
+    try:
+        return kernel_sources_sha(os.path.join(tree, "physically_based_renderer_amd", "csrc"))
+    finally:
+        nat.HEADER_PATH = saved
+
+
 def find(pattern):
     hits = sorted(glob.glob(pattern, recursive=True))
     if not hits:
@@ -26,12 +41,18 @@ def find(pattern):
     return hits[0]
 
 
-def per_kernel(path, kernel="shade_tile"):
+# The --pmc passes run bench.py --steps 5 --warmup 1 --ramp-ms 0 (profile_round.sh): the workload's launches are
+# the first six shading dispatches; later ones (the N = 1 line's config-5 scale anchor) are another workload.
+PMC_LAUNCHES = 6
+
+
+def per_kernel(path, kernel=("shade_tile", "shade_lean"), launches=PMC_LAUNCHES):
     vals = {}
     with open(path) as f:
-        for row in csv.DictReader(f):
-            if kernel not in row.get("Kernel_Name", row.get("Name", "")):
-                continue
+        rows = [r for r in csv.DictReader(f) if any(k in r.get("Kernel_Name", r.get("Name", "")) for k in kernel)]
+    dispatches = sorted({int(r["Dispatch_Id"]) for r in rows})[:launches]
+    for row in rows:
+        if int(row["Dispatch_Id"]) in dispatches:
             vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
@@ -68,7 +89,7 @@ def main():
         "source": f"profiles/{dst_tag}/pmc_*_{workload}.csv (rocprofv3 --pmc, separate passes, bench.py --steps 5)",
         "kernel_revision": revision,
         # bench.py quotes traffic / valu_issue_busy only while the kernel sources still hash to this
-        "kernel_sources_sha": kernel_sources_sha(),
+        "kernel_sources_sha": profiled_sources_sha(),
     }
     # Kernel trace of the bench run itself: mean launch time over the timed steps (the last K launches;
     # the clock-ramp and warm-up launches come first) next to the bench's own HIP-event average.
@@ -76,7 +97,7 @@ def main():
     shutil.copy(trace, os.path.join(dst, f"kernel_trace_{workload}.csv"))
     with open(trace) as f:
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in csv.DictReader(f)
-                if "shade_tile" in r["Kernel_Name"]]
+                if "shade_tile" in r["Kernel_Name"] or "shade_lean" in r["Kernel_Name"]]
     bench = None
     for line in open(os.path.join(src, "kt.log")):
         if line.startswith("{"):
