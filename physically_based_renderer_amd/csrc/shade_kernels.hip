@@ -472,11 +472,10 @@ __device__ __forceinline__ float reinhard(float c, bool fast) {
 // the IEEE quotient does) and the gamma encode of pow_inv_gamma_faithful.
 __device__ __forceinline__ float reinhard_faithful(float c) { return c * __builtin_amdgcn_rcpf(c + 1.0f); }
 
-template <int AMBIENT, bool APPLY_AO>
-__device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float ao, f3 direct, const PassArgs& ps,
-                                               const float4* __restrict__ env, bool fast, bool faithful = false) {
+// The ambient term of Default.hlsl:139-150 (before the AO extension).
+template <int AMBIENT>
+__device__ __forceinline__ f3 ambient_term(const PixelInvariants& p, const PassArgs& ps, const float4* __restrict__ env) {
     const PixelInvariants& q = p;
-    f3 ambient;
     if (AMBIENT == kAmbientIblDiffuse) {
         // Default.hlsl:141-146: kS = FresnelSchlick(N, V, F0); kD = (1 - kS)(1 - metallic);
         // irradiance = env.Sample(linear-wrap, WorldToSkyUV(N)); ambient = kD * (irradiance * albedo)
@@ -489,11 +488,16 @@ __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float a
         world_to_sky_uv(p.n, su, sv);
         const f3 irr = sample_linear_wrap(env, ps.env_w, ps.env_h, su, sv);
         const f3 diffuse = mk3(irr.x * p.albedo.x, irr.y * p.albedo.y, irr.z * p.albedo.z);
-        ambient = mk3(kd.x * diffuse.x, kd.y * diffuse.y, kd.z * diffuse.z);
-    } else {
-        // g_AmbientLight * diffuseAlbedo  (Default.hlsl:150)
-        ambient = mk3(ps.ambient[0] * p.albedo.x, ps.ambient[1] * p.albedo.y, ps.ambient[2] * p.albedo.z);
+        return mk3(kd.x * diffuse.x, kd.y * diffuse.y, kd.z * diffuse.z);
     }
+    // g_AmbientLight * diffuseAlbedo  (Default.hlsl:150)
+    return mk3(ps.ambient[0] * p.albedo.x, ps.ambient[1] * p.albedo.y, ps.ambient[2] * p.albedo.z);
+}
+
+// The rest of the PS from the ambient term: AO (extension), + direct, Reinhard, gamma (Default.hlsl:150-160).
+template <bool APPLY_AO>
+__device__ __forceinline__ float4 finish_lit(f3 ambient, float ao, f3 direct, const PassArgs& ps, bool fast,
+                                             bool faithful) {
     if (APPLY_AO) ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
     f3 lit = add3(ambient, direct);
     if (faithful) {  // wave-uniform
@@ -506,16 +510,28 @@ __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float a
                        ps.opacity);
 }
 
+template <int AMBIENT, bool APPLY_AO>
+__device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float ao, f3 direct, const PassArgs& ps,
+                                               const float4* __restrict__ env, bool fast, bool faithful = false) {
+    return finish_lit<APPLY_AO>(ambient_term<AMBIENT>(p, ps, env), ao, direct, ps, fast, faithful);
+}
+
 // The sky pass for a background pixel (Skybox.hlsl:37-49): sampleCoord = normalize(PosW);
-// WorldToSkyUV; g_SkyArray[0].Sample(linear-wrap); Reinhard; gamma; alpha 1.
-__device__ __forceinline__ float4 sky_pixel(f3 dir, const PassArgs& ps, const float4* __restrict__ sky, bool fast) {
+// WorldToSkyUV; g_SkyArray[0].Sample(linear-wrap); Reinhard; gamma; alpha 1. sky_colour is the sampled colour,
+// sky_finish the rest.
+__device__ __forceinline__ f3 sky_colour(f3 dir, const PassArgs& ps, const float4* __restrict__ sky) {
     const f3 c = normalize3(dir);
     float u, v;
     world_to_sky_uv(c, u, v);
-    f3 col = sample_linear_wrap(sky, ps.sky_w, ps.sky_h, u, v);
+    return sample_linear_wrap(sky, ps.sky_w, ps.sky_h, u, v);
+}
+__device__ __forceinline__ float4 sky_finish(f3 col, bool fast) {
     col = mk3(reinhard(col.x, fast), reinhard(col.y, fast), reinhard(col.z, fast));
     return make_float4(pow_inv_gamma(col.x), pow_inv_gamma(col.y), pow_inv_gamma(col.z),
                        1.0f);
+}
+__device__ __forceinline__ float4 sky_pixel(f3 dir, const PassArgs& ps, const float4* __restrict__ sky, bool fast) {
+    return sky_finish(sky_colour(dir, ps, sky), fast);
 }
 
 // D3D FLOAT -> UNORM8 (the R8G8B8A8_UNORM back buffer, d3dApp.h:124): NaN -> 0, clamp to [0, 1],
@@ -563,6 +579,120 @@ __device__ __forceinline__ int lane_id_fresh() {
 }
 
 }  // namespace
+
+// The IEEE light sum of ONE pixel (wave-uniform `q`, `pos`) with the wave's lanes splitting the lights: lane l
+// evaluates light base + l (point_or_spot_light / directional_light, the functions lighting_exact_wave calls),
+// and the terms are then added in light order from +0 -- directional, point, spot, as the reference's
+// ComputeLighting loops (LightingUtil.hlsl:176-199). An unlit light's term is +0, which leaves the sum as it is
+// (it starts at +0 and is never -0), exactly as lighting_exact_wave's skipped addition. One evaluation of a
+// light's sequence per 64 lights instead of one per light: a wave with a handful of pixels to re-pass finishes
+// in a fraction of the serial loop's time (those waves were the stragglers of short launches).
+__device__ __forceinline__ f3 lighting_exact_lanes(const PixelInvariants& q, f3 pos, const float4* __restrict__ lights,
+                                                   const PassArgs& ps) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int n = ps.n_dir + ps.n_point + ps.n_spot, sp_begin = ps.n_dir + ps.n_point;
+    f3 sum = mk3(0.0f, 0.0f, 0.0f);
+    for (int base = 0; base < n; base += 64) {
+        const int j = base + lane;
+        f3 t = mk3(0.0f, 0.0f, 0.0f);
+        bool unused = true;
+        if (j < n) {
+            const float4 r0 = lights[3 * j], r1 = lights[3 * j + 1], r2 = lights[3 * j + 2];
+            if (j < ps.n_dir) {
+                t = directional_light<false>(q, r0, r1, unused);
+            } else {
+                f3 c;
+                const bool lit = j >= sp_begin ? point_or_spot_light<true, false>(q, pos, r0, r1, r2, c, unused)
+                                               : point_or_spot_light<false, false>(q, pos, r0, r1, r2, c, unused);
+                if (lit) t = c;
+            }
+        }
+        const int cnt = min(64, n - base);
+        for (int k = 0; k < cnt; ++k) {
+            sum.x = sum.x + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.x), k));
+            sum.y = sum.y + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.y), k));
+            sum.z = sum.z + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.z), k));
+        }
+    }
+    return sum;
+}
+
+// One pixel (G-buffer index `idx`) with the compiler's IEEE sequences: V, the BRDF invariants, the light sum in
+// the reference's order (lighting_exact_wave: every light, no culling) and the finish (faithful_finish: the
+// faithful wave's finish of a re-passed pixel). Wave-uniform call; lanes with !need return zeros.
+// LANES: `idx` is wave-uniform and the lanes split the lights (lighting_exact_lanes); otherwise every lane with
+// `need` shades its own pixel.
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool LANES>
+__device__ __forceinline__ float4 shade_pixel_exact(const GBufferArgs& gb, const PassArgs& ps,
+                                                    const float4* __restrict__ lights, const float4* __restrict__ env,
+                                                    int64_t idx, bool need, bool faithful_finish) {
+    if (!LANES) idx = need ? idx : 0;
+    const f3 pos = mk3(gb.plane[0][idx], gb.plane[1][idx], gb.plane[2][idx]);
+    const f3 n = mk3(gb.plane[3][idx], gb.plane[4][idx], gb.plane[5][idx]);
+    const f3 albedo = mk3(gb.plane[6][idx], gb.plane[7][idx], gb.plane[8][idx]);
+    const float metallic = gb.plane[9][idx], roughness = gb.plane[10][idx];
+    const float ao = APPLY_AO ? gb.plane[11][idx] : 1.0f;
+    // F0 exactly as load_pair forms it (Default.hlsl:92-95).
+    const f3 f0 = F0_PLANE ? mk3(gb.plane[12][idx], gb.plane[13][idx], gb.plane[14][idx])
+                           : mk3(ps.fresnel_r0[0] + metallic * (albedo.x - ps.fresnel_r0[0]),
+                                 ps.fresnel_r0[1] + metallic * (albedo.y - ps.fresnel_r0[1]),
+                                 ps.fresnel_r0[2] + metallic * (albedo.z - ps.fresnel_r0[2]));
+    const f3 eye = mk3(ps.eye[0], ps.eye[1], ps.eye[2]);
+    const PixelInvariants q = make_invariants(n, normalize3(sub3(eye, pos)), albedo, f0, metallic, roughness);
+    f3 d, unused;
+    if (LANES)
+        d = lighting_exact_lanes(q, pos, lights, ps);
+    else
+        lighting_exact_wave(q, q, pos, pos, need, false, lights, ps, d, unused);
+    return finish_pixel<AMBIENT, APPLY_AO>(q, ao, d, ps, env, false, faithful_finish);
+}
+
+// A wave re-passes up to this many pixels one at a time with the lanes splitting the lights (each costs about
+// one light's IEEE sequence plus the ordered adds); more, and every lane takes its own pixels.
+constexpr int kLanesRepassMax = 8;
+
+// The exact re-pass of one wave's pixels (need_a / need_b: the pair's elements), after the wave has stored
+// everything else: each pixel is read back from the G-buffer and evaluated with the IEEE sequences
+// (shade_pixel_exact; `faithful`: the finish of a faithful wave), so nothing of the fast path is live here.
+// Up to kLanesRepassMax pixels go one at a time with the lanes splitting the lights; more, and every lane
+// takes its own pixels.
+template <int AMBIENT, bool F0_PLANE, bool APPLY_AO>
+__device__ __forceinline__ void repass_exact(const GBufferArgs& gb, const PassArgs& ps,
+                                             const float4* __restrict__ lights, const float4* __restrict__ env,
+                                             const FrameArgs& fr, int tile_x, int tile_y, int wave_id, bool need_a,
+                                             bool need_b, int n_exact, bool faithful) {
+    const int tid = threadIdx.x & 63;
+    if (n_exact <= kLanesRepassMax) {
+        uint64_t ma = lanes(need_a), mb = lanes(need_b);
+        while ((ma | mb) != 0) {
+            const bool second = ma == 0;
+            uint64_t& m = second ? mb : ma;
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            const int rx = tile_x * kTileW + 2 * (l & 31) + (second ? 1 : 0);
+            const int ry = tile_y * kTileH + 2 * wave_id + (l >> 5);
+            float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, true>(gb, ps, lights, env,
+                                                                            (int64_t)ry * gb.row_stride + rx, true,
+                                                                            faithful);
+            if (tid == 0 && alpha_keep(gb, (int64_t)ry * gb.row_stride + rx, c))
+                store_pixel(fr, (int64_t)ry * fr.out_stride + rx, c);
+        }
+    } else {
+        const int ln = lane_id_fresh();
+        const int rx = tile_x * kTileW + 2 * (ln & 31);
+        const int ry = tile_y * kTileH + 2 * wave_id + (ln >> 5);
+        const int64_t gi = (int64_t)ry * gb.row_stride + rx, oi = (int64_t)ry * fr.out_stride + rx;
+        if (lanes(need_a) != 0) {
+            float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi, need_a, faithful);
+            if (need_a && alpha_keep(gb, gi, c)) store_pixel(fr, oi, c);
+        }
+        if (lanes(need_b) != 0) {
+            float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi + 1, need_b,
+                                                                             faithful);
+            if (need_b && alpha_keep(gb, gi + 1, c)) store_pixel(fr, oi + 1, c);
+        }
+    }
+}
 
 // BAL (untiled only; PassArgs::balanced): the variant whose lean waves take the wave-balanced point-light lists
 // (pbr_balanced.h) -- 1: faithful passes, 2: exact passes; separate instantiations so that the other variants'
@@ -833,76 +963,6 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 // (FAITHFUL: the pass has PBR_FLAG_FAITHFUL) carries no faithful code in the exact-mode one. Frames and pass
 // statistics are bit-identical to shade_tile_kernel's (tests/test_gpu_lean.py).
 
-// The IEEE light sum of ONE pixel (wave-uniform `q`, `pos`) with the wave's lanes splitting the lights: lane l
-// evaluates light base + l (point_or_spot_light / directional_light, the functions lighting_exact_wave calls),
-// and the terms are then added in light order from +0 -- directional, point, spot, as the reference's
-// ComputeLighting loops (LightingUtil.hlsl:176-199). An unlit light's term is +0, which leaves the sum as it is
-// (it starts at +0 and is never -0), exactly as lighting_exact_wave's skipped addition. One evaluation of a
-// light's sequence per 64 lights instead of one per light: a wave with a handful of pixels to re-pass finishes
-// in a fraction of the serial loop's time (those waves were the stragglers of short launches).
-__device__ __forceinline__ f3 lighting_exact_lanes(const PixelInvariants& q, f3 pos, const float4* __restrict__ lights,
-                                                   const PassArgs& ps) {
-    const int lane = (int)(threadIdx.x & 63);
-    const int n = ps.n_dir + ps.n_point + ps.n_spot, sp_begin = ps.n_dir + ps.n_point;
-    f3 sum = mk3(0.0f, 0.0f, 0.0f);
-    for (int base = 0; base < n; base += 64) {
-        const int j = base + lane;
-        f3 t = mk3(0.0f, 0.0f, 0.0f);
-        bool unused = true;
-        if (j < n) {
-            const float4 r0 = lights[3 * j], r1 = lights[3 * j + 1], r2 = lights[3 * j + 2];
-            if (j < ps.n_dir) {
-                t = directional_light<false>(q, r0, r1, unused);
-            } else {
-                f3 c;
-                const bool lit = j >= sp_begin ? point_or_spot_light<true, false>(q, pos, r0, r1, r2, c, unused)
-                                               : point_or_spot_light<false, false>(q, pos, r0, r1, r2, c, unused);
-                if (lit) t = c;
-            }
-        }
-        const int cnt = min(64, n - base);
-        for (int k = 0; k < cnt; ++k) {
-            sum.x = sum.x + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.x), k));
-            sum.y = sum.y + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.y), k));
-            sum.z = sum.z + __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.z), k));
-        }
-    }
-    return sum;
-}
-
-// One pixel (G-buffer index `idx`) with the compiler's IEEE sequences: V, the BRDF invariants, the light sum in
-// the reference's order (lighting_exact_wave: every light, no culling) and the finish (faithful_finish: the
-// faithful wave's finish of a re-passed pixel). Wave-uniform call; lanes with !need return zeros.
-// LANES: `idx` is wave-uniform and the lanes split the lights (lighting_exact_lanes); otherwise every lane with
-// `need` shades its own pixel.
-template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool LANES>
-__device__ __forceinline__ float4 shade_pixel_exact(const GBufferArgs& gb, const PassArgs& ps,
-                                                    const float4* __restrict__ lights, const float4* __restrict__ env,
-                                                    int64_t idx, bool need, bool faithful_finish) {
-    if (!LANES) idx = need ? idx : 0;
-    const f3 pos = mk3(gb.plane[0][idx], gb.plane[1][idx], gb.plane[2][idx]);
-    const f3 n = mk3(gb.plane[3][idx], gb.plane[4][idx], gb.plane[5][idx]);
-    const f3 albedo = mk3(gb.plane[6][idx], gb.plane[7][idx], gb.plane[8][idx]);
-    const float metallic = gb.plane[9][idx], roughness = gb.plane[10][idx];
-    const float ao = APPLY_AO ? gb.plane[11][idx] : 1.0f;
-    // F0 exactly as load_pair forms it (Default.hlsl:92-95).
-    const f3 f0 = F0_PLANE ? mk3(gb.plane[12][idx], gb.plane[13][idx], gb.plane[14][idx])
-                           : mk3(ps.fresnel_r0[0] + metallic * (albedo.x - ps.fresnel_r0[0]),
-                                 ps.fresnel_r0[1] + metallic * (albedo.y - ps.fresnel_r0[1]),
-                                 ps.fresnel_r0[2] + metallic * (albedo.z - ps.fresnel_r0[2]));
-    const f3 eye = mk3(ps.eye[0], ps.eye[1], ps.eye[2]);
-    const PixelInvariants q = make_invariants(n, normalize3(sub3(eye, pos)), albedo, f0, metallic, roughness);
-    f3 d, unused;
-    if (LANES)
-        d = lighting_exact_lanes(q, pos, lights, ps);
-    else
-        lighting_exact_wave(q, q, pos, pos, need, false, lights, ps, d, unused);
-    return finish_pixel<AMBIENT, APPLY_AO>(q, ao, d, ps, env, false, faithful_finish);
-}
-
-// A wave re-passes up to this many pixels one at a time with the lanes splitting the lights (each costs about
-// one light's IEEE sequence plus the ordered adds); more, and every lane takes its own pixels.
-constexpr int kLanesRepassMax = 8;
 
 // One wave's 64x2 pixels: wave wave_id (tile rows 2 wave_id, 2 wave_id + 1) of tile (tile_x, tile_y), statistics
 // slot wave_global. The caller has staged the powf tables.
@@ -1029,38 +1089,9 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         st[kStatGeometryPixels] = geo_px;
         st[kStatBackfaceTests] = 0;
     }
-    if (n_exact != 0) {  // wave-uniform, rare: the IEEE path
-        if (n_exact <= kLanesRepassMax) {  // pixel by pixel, the lanes splitting the lights
-            uint64_t ma = lanes(need_a), mb = lanes(need_b);
-            while ((ma | mb) != 0) {
-                const bool second = ma == 0;
-                uint64_t& m = second ? mb : ma;
-                const int l = __builtin_ctzll(m);
-                m &= m - 1;
-                const int rx = tile_x * kTileW + 2 * (l & 31) + (second ? 1 : 0);
-                const int ry = tile_y * kTileH + 2 * wave_id + (l >> 5);
-                float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, true>(
-                    gb, ps, lights, env, (int64_t)ry * gb.row_stride + rx, true, faithful_wave);
-                if (tid == 0 && alpha_keep(gb, (int64_t)ry * gb.row_stride + rx, c))
-                    store_pixel(fr, (int64_t)ry * fr.out_stride + rx, c);
-            }
-        } else {  // one pixel of the pair at a time, each lane its own
-            const int ln = lane_id_fresh();
-            const int rx = tile_x * kTileW + 2 * (ln & 31);
-            const int ry = tile_y * kTileH + 2 * wave_id + (ln >> 5);
-            const int64_t gi = (int64_t)ry * gb.row_stride + rx, oi = (int64_t)ry * fr.out_stride + rx;
-            if (lanes(need_a) != 0) {
-                float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi, need_a,
-                                                                                 faithful_wave);
-                if (need_a && alpha_keep(gb, gi, c)) store_pixel(fr, oi, c);
-            }
-            if (lanes(need_b) != 0) {
-                float4 c = shade_pixel_exact<AMBIENT, F0_PLANE, APPLY_AO, false>(gb, ps, lights, env, gi + 1,
-                                                                                 need_b, faithful_wave);
-                if (need_b && alpha_keep(gb, gi + 1, c)) store_pixel(fr, oi + 1, c);
-            }
-        }
-    }
+    if (n_exact != 0)  // wave-uniform, rare: the IEEE path
+        repass_exact<AMBIENT, F0_PLANE, APPLY_AO>(gb, ps, lights, env, fr, tile_x, tile_y, wave_id, need_a, need_b,
+                                                  n_exact, faithful_wave);
     TL_FLAGS((n_exact != 0 ? 1 : 0) | (FAITHFUL && !faithful_wave ? 2 : 0));
     TL_END(wave_global);
 }
