@@ -563,6 +563,17 @@ __device__ __forceinline__ bool alpha_keep(const GBufferArgs& gb, int64_t gidx, 
     return true;
 }
 
+// alpha_keep for the pixel pair at G-buffer row offset `grow` (ga / gb_: geometry), in one uniform branch that
+// passes without the flag: the stores of an ordinary pass see no extra work or live values.
+__device__ __forceinline__ void alpha_keep_pair(const GBufferArgs& gb, int64_t grow, bool ga, bool gb_, float4& ca,
+                                                float4& cb, bool& keep_a, bool& keep_b) {
+    keep_a = keep_b = true;
+    if (__builtin_expect(gb.alpha_test, 0)) {
+        if (ga) keep_a = alpha_keep(gb, grow, ca);
+        if (gb_) keep_b = alpha_keep(gb, grow + 1, cb);
+    }
+}
+
 // Coverage of a pixel: geometry unless the frame has a coverage plane holding 0 there.
 __device__ __forceinline__ bool is_geometry(const FrameArgs& fr, int x, int y) {
     return fr.coverage == nullptr || fr.coverage[(int64_t)y * fr.coverage_stride + x] != 0;
@@ -938,17 +949,18 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             if (vb) ao_b = gb.plane[11][arow + 1];
         }
     }
-    const int64_t grow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
-    if (va) {
-        float4 c = ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
-                      : sky_pixel(ua.n, ps, fr.sky, !exact_only);
-        if (!ga || alpha_keep(gb, grow, c)) store_pixel(fr, orow, c);
-    }
-    if (vb) {
-        float4 c = gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
-                       : sky_pixel(ub.n, ps, fr.sky, !exact_only);
-        if (!gb_ || alpha_keep(gb, grow + 1, c)) store_pixel(fr, orow + 1, c);
-    }
+    float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca;
+    if (va)
+        ca = ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
+                : sky_pixel(ua.n, ps, fr.sky, !exact_only);
+    if (vb)
+        cb = gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
+                 : sky_pixel(ub.n, ps, fr.sky, !exact_only);
+    bool keep_a, keep_b;
+    alpha_keep_pair(gb, (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx, ga, gb_, ca,
+                    cb, keep_a, keep_b);
+    if (va && keep_a) store_pixel(fr, orow, ca);
+    if (vb && keep_b) store_pixel(fr, orow + 1, cb);
     TL_END(((long long)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id);
 }
 
@@ -1066,15 +1078,16 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
                     if (vb) ao_b = gb.plane[11][arow + 1];
                 }
             }
-            const int64_t grow = (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
-            if (va && !need_a) {
-                float4 c = finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, lane(d2, 0), ps, env, ok_a, faithful_wave);
-                if (alpha_keep(gb, grow, c)) store_pixel(fr, orow, c);
-            }
-            if (vb && !need_b) {
-                float4 c = finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, lane(d2, 1), ps, env, ok_b, faithful_wave);
-                if (alpha_keep(gb, grow + 1, c)) store_pixel(fr, orow + 1, c);
-            }
+            float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca;
+            if (va && !need_a)
+                ca = finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, lane(d2, 0), ps, env, ok_a, faithful_wave);
+            if (vb && !need_b)
+                cb = finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, lane(d2, 1), ps, env, ok_b, faithful_wave);
+            bool keep_a, keep_b;
+            alpha_keep_pair(gb, (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx,
+                            va && !need_a, vb && !need_b, ca, cb, keep_a, keep_b);
+            if (va && !need_a && keep_a) store_pixel(fr, orow, ca);
+            if (vb && !need_b && keep_b) store_pixel(fr, orow + 1, cb);
         }
     }
     const int n_exact = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
