@@ -204,14 +204,34 @@ __device__ __forceinline__ bool light_survives(float4 lp, const TileBounds& wb) 
 // The number of light terms the wave sums under tiled culling: directional lights + the point/spot lights
 // that survive its box (one lane per light, the same test as the loop). PBR_FLAG_FAITHFUL's bound counts
 // summed terms, so a culled pass with more lights than the bound allows can still run it per wave.
+// The survivor masks of lights [base, base + 256) of the range [.., b1): bit l of m[k] = light base + 64 k + l
+// may reach the wave's box. The four chunks' position loads are issued together before any test (a dependent load
+// per 64 lights left the wave waiting for each in turn: config 4's per-wave term count and culled walk).
+__device__ __forceinline__ void survivor_masks(const float4* __restrict__ lights, int base, int b1,
+                                               const TileBounds& wb, bool cull_enabled, uint64_t (&m)[4]) {
+    const int lane = (int)(threadIdx.x & 63);
+    float4 lp[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = base + 64 * k + lane;
+        lp[k] = j < b1 && cull_enabled ? lights[3 * j + 2] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = base + 64 * k + lane;
+        m[k] = lanes(j < b1 && (!cull_enabled || light_survives(lp[k], wb)));
+    }
+}
+
 __device__ __forceinline__ int wave_light_terms(const float4* __restrict__ lights, const PassArgs& ps,
                                                 const TileBounds& wb, bool cull_enabled) {
     const int b0 = ps.n_dir, b1 = ps.n_dir + ps.n_point + ps.n_spot;
     if (!cull_enabled) return b1;
     int total = ps.n_dir;
-    for (int base = b0; base < b1; base += 64) {
-        const int j = base + (int)(threadIdx.x & 63);
-        total += __popcll(lanes(j < b1 && light_survives(lights[3 * j + 2], wb)));
+    for (int base = b0; base < b1; base += 256) {
+        uint64_t m[4];
+        survivor_masks(lights, base, b1, wb, true, m);
+        total += __popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]);
     }
     return total;
 }
@@ -272,16 +292,18 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
             for (int j = b0; j < b1; ++j) point(j);
             return;
         }
-        for (int base = b0; base < b1; base += 64) {
-            const int j = base + (int)(threadIdx.x & 63);
-            bool keep = j < b1;
-            if (keep && cull_enabled) keep = light_survives(lights[3 * j + 2], wb);
-            uint64_t m = lanes(keep);
-            kept_total += __popcll(m);
-            while (m) {
-                const int jl = base + __builtin_ctzll(m);
-                m &= m - 1;
-                point(jl);
+        for (int base = b0; base < b1; base += 256) {
+            uint64_t ms[4];
+            survivor_masks(lights, base, b1, wb, cull_enabled, ms);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint64_t m = ms[k];
+                kept_total += __popcll(m);
+                while (m) {
+                    const int jl = base + 64 * k + __builtin_ctzll(m);
+                    m &= m - 1;
+                    point(jl);
+                }
             }
         }
     };
