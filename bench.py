@@ -42,6 +42,12 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, vector FP32 (spec)
 # base 27 + 20 hoisted BRDF invariants + 91 per point light + 87 for the diffuse IBL.
 FLOP_BASE, FLOP_HOIST, FLOP_POINT, FLOP_IBL = 27, 20, 91, 87
 FLOP_RANGE_TEST = 9  # per light and tile under tiled culling (box distance + compare)
+# The north-star parity bar: RGBA within 1e-5 relative fp32 per channel of the reference CPU evaluation (NaN where
+# it has NaN). RGBA8 output: a 1e-5 relative difference can move a code by one where c * 255 + 0.5 sits on an
+# integer, so codes may differ by at most 1.
+PARITY_REL_TOL = 1e-5
+PARITY_RGBA8_CODE_TOL = 1
+EXIT_PARITY = 3  # bench.py's exit status when the checked frame misses the bar (no metric line is printed)
 
 
 def log(*a):
@@ -179,6 +185,44 @@ def parity_of(got, ref, rgba8: bool) -> dict:
                 "parity_bit_exact_frac": round(float((d == 0).mean()) if d.size else 1.0, 6)}
     return {"parity_max_rel": float(O.rel_err(got, ref).max()) if got.size else 0.0,
             "parity_bit_exact_frac": round(float(O.bit_equal(got, ref).mean()) if got.size else 1.0, 6)}
+
+
+def parity_failures(line: dict) -> list:
+    """Every parity result in a bench line that misses the north-star bar: the CPU leg's frame check
+    (parity_max_rel / parity_max_code_diff; a NaN where the reference has none, or the reverse, is an infinite
+    relative error), the exact leg's, the assembled frame's at N > 1 and its band checksums. Empty = all pass."""
+    bad = []
+
+    def check(where: str, p: dict):
+        rel, code = p.get("parity_max_rel"), p.get("parity_max_code_diff")
+        if rel is not None and not rel <= PARITY_REL_TOL:  # NaN-safe: NaN or inf fails
+            bad.append(f"{where}parity_max_rel {rel} > {PARITY_REL_TOL}")
+        if code is not None and not code <= PARITY_RGBA8_CODE_TOL:
+            bad.append(f"{where}parity_max_code_diff {code} > {PARITY_RGBA8_CODE_TOL}")
+
+    check("", line)
+    if isinstance(line.get("exact_mode"), dict):
+        check("exact_mode.", line["exact_mode"])
+    if isinstance(line.get("gathered_frame_parity"), dict):
+        check("gathered_frame_parity.", line["gathered_frame_parity"])
+    if line.get("gather_checksums_match") is False:
+        bad.append("gather_checksums_match false")
+    return bad
+
+
+def emit_line(line: dict) -> int:
+    """Print the bench line on stdout and return 0 -- unless a parity check in it failed: then the line goes to
+    stderr with the failures, nothing is printed on stdout (no throughput is published for a wrong frame) and the
+    exit status is EXIT_PARITY."""
+    bad = parity_failures(line)
+    checked = any(k in line for k in ("parity_max_rel", "parity_max_code_diff", "gathered_frame_parity"))
+    line = {**line, "parity_checked": checked, "parity_ok": not bad if checked else None}
+    if bad:
+        log("PARITY FAILURE: " + "; ".join(bad))
+        print(json.dumps({**line, "parity_failures": bad}), file=sys.stderr, flush=True)
+        return EXIT_PARITY
+    print(json.dumps(line), flush=True)
+    return 0
 
 
 def cpu_baseline(cfg, planes_host, pc, env, gpu_frame, budget_rows: int, kind: str = "auto", rgba8: bool = False):
@@ -333,6 +377,21 @@ def shade_steps(shade_into, outs, stream, warmup: int, steps: int, gather=None, 
     return time.perf_counter() - t_start, [a.elapsed_time(b) for a, b in events]
 
 
+def clock_ramp(shade_into, out, ramp_ms: float) -> dict:
+    """Untimed back-to-back shading passes for `ramp_ms` (synchronised every 8 launches), so that timed steps run
+    at settled GPU clocks (the kernel trace shows the clock ramping over the first ~40 ms of launches). Not a step."""
+    t0 = time.perf_counter()
+    n = 0
+    while ramp_ms > 0:
+        shade_into(out)
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize()
+            if time.perf_counter() - t0 >= ramp_ms / 1e3:
+                break
+    return {"ms": round((time.perf_counter() - t0) * 1e3, 1), "launches": n}
+
+
 def band_anchor(ctx, args, world: int, device, stream, resident=None) -> dict:
     """The scaling anchor: ONE rank's config-5 band (8192 x rows_per_rank, RGBA8, the run's mode) shaded alone
     -- no gather, no other rank -- timed like a step. It is the per-GPU work of every point of the 1/2/4/8-GPU
@@ -352,11 +411,14 @@ def band_anchor(ctx, args, world: int, device, stream, resident=None) -> dict:
     def shade_into(o):
         ctx.shade_frame(gb, o, fmt=N.PBR_OUTPUT_RGBA8_UNORM, stream=stream)
 
+    # The same clock ramp as the headline before the warm-up: the anchor is timed at settled clocks like every
+    # point of the curve it anchors (measured cold, it read 6% low and overstated efficiency_vs_anchor).
+    ramp = clock_ramp(shade_into, outs[0], args.ramp_ms)
     wall, ms = shade_steps(shade_into, outs, stream, max(args.warmup, 3), args.steps)
     px = cfg5.width * rows
     return {"workload": f"{cfg5.name}_band{rows}", "output": "rgba8", "mode": args.mode, "px_per_step": px,
             "value": round(px * args.steps / wall / 1e6, 2), "ms_per_step": round(wall / args.steps * 1e3, 4),
-            "shade_ms": round(float(np.mean(ms)), 4)}
+            "shade_ms": round(float(np.mean(ms)), 4), "clock_ramp": ramp}
 
 
 def main():
@@ -399,6 +461,9 @@ def main():
                          "C restatement (oracle/pbr_oracle.c); auto = the reference build when present")
     ap.add_argument("--cpu-rows", type=int, default=0,
                     help="rows in the CPU-baseline sample (0 = the whole frame or band)")
+    ap.add_argument("--inject-parity-breach", type=float, default=0.0, metavar="REL",
+                    help="test only: scale one channel of the checked frame by (1 + REL) before the parity check, "
+                         "to show that a frame off the 1e-5 bar is refused (exit status 3, no metric line)")
     ap.add_argument("--parity-rows", type=int, default=8,
                     help="N > 1: rows per band of the assembled frame checked against the oracle (0 = none)")
     args = ap.parse_args()
@@ -450,16 +515,7 @@ def main():
             ctx.shade(gb, o, stream)
 
     # GPU clock ramp (see --ramp-ms): full shading passes, untimed, before the W warm-up steps.
-    t_ramp = time.perf_counter()
-    n_ramp = 0
-    while args.ramp_ms > 0:
-        shade_into(outs[0])
-        n_ramp += 1
-        if n_ramp % 8 == 0:
-            torch.cuda.synchronize()
-            if time.perf_counter() - t_ramp >= args.ramp_ms / 1e3:
-                break
-    ramp_ms = (time.perf_counter() - t_ramp) * 1e3
+    ramp = clock_ramp(shade_into, outs[0], args.ramp_ms)
     elapsed, kernel_ms = shade_steps(shade_into, outs, stream, args.warmup, args.steps, gather, in_group)
 
     # The executed work of the last timed pass (pbr_last_pass_stats; every timed pass shades the same input).
@@ -562,18 +618,13 @@ def main():
         parity = {}
         exact_leg = None
         frame = outs[0][: band.rows].cpu().numpy() if world == 1 else None  # the timed mode's frame
+        if frame is not None and args.inject_parity_breach:
+            frame = frame.copy()
+            frame.reshape(-1)[1] = frame.reshape(-1)[1] * (1.0 + args.inject_parity_breach) if not rgba8 else 255
         exact_frame = None
-        if world == 1 and args.mode == "faithful" and args.exact_leg:
-            exact_leg = time_exact_mode(ctx, pc, gb, outs[0], stream, args, fmt, rgba8, band_px)
-            exact_frame = outs[0][: band.rows].cpu().numpy()
-        if world == 1 and not args.no_cpu_baseline:
-            cpu, parity, (step_, ref) = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows,
-                                                    args.cpu_kind, rgba8)
-            if exact_frame is not None:
-                exact_leg.update(parity_of(exact_frame[::step_], ref, rgba8))
-        elif world > 1 and gather is not None and args.parity_rows > 0:
-            parity = {"gathered_frame_parity": gathered_parity(cfg, pc, env, gather.assembled(cfg.height).cpu().numpy(),
-                                                               world, args.parity_rows, rgba8)}
+        assembled = gather.assembled(cfg.height).cpu().numpy() if world > 1 and gather is not None else None
+        # The scaling anchor runs right after the timed steps, on a warm GPU, before the host-side legs (the CPU
+        # baseline and the parity checks leave the GPU idle for seconds); it ramps the clock itself as well.
         scale = {}
         if not args.no_anchor:
             anchor = band_anchor(ctx, args, world, device, stream, (gb, outs) if banded and rgba8 else None)
@@ -582,9 +633,23 @@ def main():
                 per_rank = value / world
                 scale.update({"per_rank_mpix_s": round(per_rank, 2),
                               "efficiency_vs_anchor": round(per_rank / anchor["value"], 4)})
+            ctx.set_pass(pc, stream)  # the anchor set its own pass (config 5 geometry, same lights and mode)
+            if env is not None:
+                ctx.set_env_map(env, stream)
+        if world == 1 and args.mode == "faithful" and args.exact_leg:
+            exact_leg = time_exact_mode(ctx, pc, gb, outs[0], stream, args, fmt, rgba8, band_px)
+            exact_frame = outs[0][: band.rows].cpu().numpy()
+        if world == 1 and not args.no_cpu_baseline:
+            cpu, parity, (step_, ref) = cpu_baseline(cfg, staging.numpy(), pc, env, frame, args.cpu_rows,
+                                                    args.cpu_kind, rgba8)
+            if exact_frame is not None:
+                exact_leg.update(parity_of(exact_frame[::step_], ref, rgba8))
+        elif world > 1 and assembled is not None and args.parity_rows > 0:
+            parity = {"gathered_frame_parity": gathered_parity(cfg, pc, env, assembled, world, args.parity_rows,
+                                                               rgba8)}
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpix/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "clock_ramp": {"ms": round(ramp_ms, 1), "launches": n_ramp},
+            "warmup": args.warmup, "clock_ramp": ramp,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "output": output, "mode": args.mode,
             "data": "synthetic deterministic G-buffer (splitmix64 per pixel; rustediron metal/rough tiles; "
@@ -601,11 +666,14 @@ def main():
             **({"exact_mode": exact_leg} if exact_leg is not None else {}),
             "pcie_h2d_gbps": round(staging.numel() * 4 / t_upload / 1e9, 2),
         }
-        print(json.dumps(out), flush=True)
+        rc = emit_line(out)
+    else:
+        rc = 0
     ctx.close()
     if in_group:
         dist.destroy_process_group()
+    return rc
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

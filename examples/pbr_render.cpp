@@ -97,6 +97,7 @@ struct Args {
     int config = 3, width = 0, height = 0, steps = 0, warmup = 3, bands = 1, threads = 0;
     int rows_per_rank = 0, print_bands = 0;
     double ramp_ms = 200.0;
+    double comm_timeout_s = 300.0;  // --comm-timeout / PBR_DIST_TIMEOUT_S: give up on a silent peer (dist.py)
     std::string output = "rgba32f", mode = "exact", dump, assets = "physically_based_renderer_amd/assets";
     std::string rendezvous;
     bool check_assets = false, rccl = false;
@@ -104,6 +105,7 @@ struct Args {
 
 Args parse(int argc, char** argv) {
     Args a;
+    if (const char* t = std::getenv("PBR_DIST_TIMEOUT_S"); t && *t) a.comm_timeout_s = std::atof(t);
     for (int i = 1; i < argc; ++i) {
         const std::string k = argv[i];
         auto val = [&]() -> std::string {
@@ -119,6 +121,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--rows-per-rank") a.rows_per_rank = std::stoi(val());
         else if (k == "--threads") a.threads = std::stoi(val());
         else if (k == "--ramp-ms") a.ramp_ms = std::stod(val());
+        else if (k == "--comm-timeout") a.comm_timeout_s = std::stod(val());
         else if (k == "--output") a.output = val();
         else if (k == "--mode") a.mode = val();
         else if (k == "--dump") a.dump = val();
@@ -194,6 +197,43 @@ ncclUniqueId rendezvous(int rank, int world, const std::string& path) {
     }
 }
 
+// Failure detection on the communicator (the reference checks GetDeviceRemovedReason around every Draw
+// step, PBRApp.cpp:247-350): a peer that died or a link error surfaces as an asynchronous RCCL error, which a
+// plain hipStreamSynchronize on the communication stream would never report -- it would block forever. Every
+// frame checks ncclCommGetAsyncError, and every wait on the communication stream polls it with a deadline; on an
+// error or a timeout the communicator is aborted (so no kernel of it keeps the GPU busy) and the run ends with a
+// message and a non-zero exit status.
+struct CommGuard {
+    ncclComm_t comm;
+    int rank;
+    double timeout_s;
+    void check(const char* where) const {
+        ncclResult_t async = ncclSuccess;
+        PBR_THROW_IF_NCCL(ncclCommGetAsyncError(comm, &async));
+        if (async != ncclSuccess && async != ncclInProgress) {
+            (void)ncclCommAbort(comm);
+            throw std::runtime_error("rank " + std::to_string(rank) + ": RCCL asynchronous error at " + where + ": " +
+                                     ncclGetErrorString(async) + " (communicator aborted)");
+        }
+    }
+    // hipStreamSynchronize(s) for a stream with RCCL work, bounded by timeout_s and watching the communicator.
+    void wait(hipStream_t s, const char* where) const {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned spin = 0;; ++spin) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) return;
+            if (q != hipErrorNotReady) PBR_THROW_IF_HIP(q);
+            check(where);
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+                (void)ncclCommAbort(comm);
+                throw std::runtime_error("rank " + std::to_string(rank) + ": " + where + " did not complete within " +
+                                         std::to_string(timeout_s) + " s (peer lost?); communicator aborted");
+            }
+            if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+};
+
 int run_ranked(const Args& args, const SceneConfig* cfg, Assets& assets) {
     const int rank = env_int("RANK", 0), world = env_int("WORLD_SIZE", 1), local = env_int("LOCAL_RANK", 0);
     if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("RANK / WORLD_SIZE out of range");
@@ -241,6 +281,7 @@ int run_ranked(const Args& args, const SceneConfig* cfg, Assets& assets) {
     ncclComm_t comm;
     const ncclUniqueId id = rendezvous(rank, world, args.rendezvous);
     PBR_THROW_IF_NCCL(ncclCommInitRank(&comm, world, id, rank));
+    const CommGuard guard{comm, rank, args.comm_timeout_s};
 
     // Two band slots (rows_max rows, the gather's fixed message size) so frame k + 1 shades while frame k is in
     // flight; rank 0 also holds the (world, rows_max, W) gather buffer.
@@ -284,17 +325,18 @@ int run_ranked(const Args& args, const SceneConfig* cfg, Assets& assets) {
         PBR_THROW_IF_HIP(hipStreamWaitEvent(comm_stream, shaded[slot], 0));
         gather(slot);
         PBR_THROW_IF_HIP(hipEventRecord(gathered[slot], comm_stream));
+        guard.check("frame gather");
     };
     // Barrier + reduction over ranks on the device (RCCL all-reduce of one value, then host sync).
     double* d_red = nullptr;
     PBR_THROW_IF_HIP(hipMalloc(reinterpret_cast<void**>(&d_red), sizeof(double)));
     auto reduce = [&](double v, ncclRedOp_t op) {
         PBR_THROW_IF_HIP(hipStreamSynchronize(shade_stream));
-        PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+        guard.wait(comm_stream, "gather");
         PBR_THROW_IF_HIP(hipMemcpyAsync(d_red, &v, sizeof v, hipMemcpyHostToDevice, comm_stream));
         PBR_THROW_IF_NCCL(ncclAllReduce(d_red, d_red, 1, ncclFloat64, op, comm, comm_stream));
         PBR_THROW_IF_HIP(hipMemcpyAsync(&v, d_red, sizeof v, hipMemcpyDeviceToHost, comm_stream));
-        PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+        guard.wait(comm_stream, "all-reduce");
         return v;
     };
     reduce(0.0, ncclSum);  // every rank has joined (and uploaded) before anything is timed
@@ -331,7 +373,7 @@ int run_ranked(const Args& args, const SceneConfig* cfg, Assets& assets) {
         while (args.ramp_ms > 0) {  // clock ramp, untimed (bench.py --ramp-ms)
             step(ramp++);
             if (ramp % 8 == 0) {
-                PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+                guard.wait(comm_stream, "gather");
                 if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count() >= args.ramp_ms) break;
             }
         }
@@ -342,7 +384,7 @@ int run_ranked(const Args& args, const SceneConfig* cfg, Assets& assets) {
         const auto ts = std::chrono::steady_clock::now();
         for (int i = 0; i < args.steps; ++i) step(i, ev[2 * i], ev[2 * i + 1]);
         PBR_THROW_IF_HIP(hipStreamSynchronize(shade_stream));
-        PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+        guard.wait(comm_stream, "gather");
         const double wall = reduce(std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count(), ncclMax);
         double shade_ms = 0;
         for (int i = 0; i < args.steps; ++i) {
@@ -356,7 +398,7 @@ int run_ranked(const Args& args, const SceneConfig* cfg, Assets& assets) {
         reduce(0.0, ncclSum);
         const auto tg = std::chrono::steady_clock::now();
         for (int i = 0; i < args.steps; ++i) gather(i & 1);
-        PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+        guard.wait(comm_stream, "gather");
         const double gather_wall = reduce(std::chrono::duration<double>(std::chrono::steady_clock::now() - tg).count(), ncclMax);
         if (rank == 0)
             std::printf("{\"tool\": \"pbr_render\", \"workload\": \"%s\", \"width\": %d, \"height\": %d, \"world\": %d, "
@@ -368,7 +410,7 @@ int run_ranked(const Args& args, const SceneConfig* cfg, Assets& assets) {
                         gather_wall / args.steps * 1e3, ramp);
     }
     PBR_THROW_IF_HIP(hipStreamSynchronize(shade_stream));
-    PBR_THROW_IF_HIP(hipStreamSynchronize(comm_stream));
+    guard.wait(comm_stream, "gather");
     PBR_THROW_IF_NCCL(ncclCommDestroy(comm));
     for (int i = 0; i < 2; ++i) {
         (void)hipEventDestroy(shaded[i]);

@@ -16,7 +16,7 @@
  *   gcc -std=c11 -O2 -D__HIP_PLATFORM_AMD__ -I include -I /opt/rocm/include examples/shade_sphere.c \
  *       -L physically_based_renderer_amd/_lib -lpbrshade -L /opt/rocm/lib -lamdhip64 -lm \
  *       -Wl,-rpath,$PWD/physically_based_renderer_amd/_lib -o build/shade_sphere
- *   build/shade_sphere [--width 640 --height 360 --out sphere.ppm --dump frame.bin]
+ *   build/shade_sphere [--width 640 --height 360 --out sphere.ppm --dump frame.bin] [--host-only]
  */
 #include <hip/hip_runtime_api.h>
 
@@ -113,11 +113,15 @@ int main(int argc, char** argv) {
     int w = 640, h = 360;
     const char* out_path = "sphere.ppm";
     const char* dump_path = NULL;
-    for (int a = 1; a + 1 < argc; a += 2) {
-        if (!strcmp(argv[a], "--width")) w = atoi(argv[a + 1]);
-        else if (!strcmp(argv[a], "--height")) h = atoi(argv[a + 1]);
-        else if (!strcmp(argv[a], "--out")) out_path = argv[a + 1];
-        else if (!strcmp(argv[a], "--dump")) dump_path = argv[a + 1];
+    int host_only = 0; /* --host-only: the host half (G-buffer + sky fill) and its checksum, no HIP call */
+    for (int a = 1; a < argc; ++a) {
+        if (!strcmp(argv[a], "--host-only")) host_only = 1;
+        else if (a + 1 >= argc) return 2;
+        else if (!strcmp(argv[a], "--width")) w = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--height")) h = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--out")) out_path = argv[++a];
+        else if (!strcmp(argv[a], "--dump")) dump_path = argv[++a];
+        else return 2;
     }
     if (w < 2 || h < 2) return 2;
     const size_t n = (size_t)w * h;
@@ -130,6 +134,14 @@ int main(int argc, char** argv) {
     if (!planes || !coverage || !frame || !sky) return 1;
     fill_gbuffer(w, h, planes, coverage);
     fill_sky(sky_w, sky_h, sky);
+    if (host_only) {
+        printf("shade_sphere: %dx%d host G-buffer fnv1a %016llx coverage %016llx sky %016llx\n", w, h,
+               (unsigned long long)fnv1a((const uint8_t*)planes, sizeof(float) * NUM_PLANES * n),
+               (unsigned long long)fnv1a(coverage, n),
+               (unsigned long long)fnv1a((const uint8_t*)sky, sizeof(uint16_t) * 4 * sky_w * sky_h));
+        free(planes), free(coverage), free(frame), free(sky);
+        return 0;
+    }
 
     /* Device buffers: the caller owns them (the library never frees them). */
     float* d_planes;

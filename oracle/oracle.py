@@ -16,7 +16,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-ORACLE_SO = os.path.join(HERE, "liboracle.so")
+# PBR_ORACLE_LIB: another build of the same C restatement (the sanitizer build of `make asan`, tests only).
+ORACLE_SO = os.environ.get("PBR_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libpbr_ref.so")
 REFERENCE_SHADER = "/root/reference/Source/Shaders/LightingUtil.hlsl"
 

@@ -53,7 +53,8 @@ constexpr int kBalRec = 7;         // float4 per exchanged pixel record
 
 // Per-wave LDS: the exchange region (one record per lane, then the 128 results) and the count histogram.
 #ifndef PBR_BAL_EXPERIMENT
-#define PBR_BAL_EXPERIMENT 0  // development timing switches (0 = product)
+#define PBR_BAL_EXPERIMENT 0  // development timing switches, bit flags (0 = product): 1 no pass 2, 2 no atan2f/asinf,
+                              // 4 no IBL block, 8 no finish, 16 no back-face tests
 #endif
 #ifndef PBR_BAL_PROFILE
 #define PBR_BAL_PROFILE 0  // development build: per-phase shader-clock sums (pbr_debug_bal_profile)
@@ -438,8 +439,13 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
         }
     };
     const int n0 = nl < 32 ? nl : 32;
+#if PBR_BAL_EXPERIMENT & 16  // development timing: no back-face tests (every other light live)
+    a0 = c0 = a1 = c1 = 0xaaaaaaaau;
+    (void)word;
+#else
     if (nl > 32) word(8, a1, c1);
     word(0, a0, c0);
+#endif
     // Live masks (light j at bit j % 32 of its word); bits above a word's light count are not lights.
     const int n1 = nl - n0;
     const uint32_t k0 = n0 == 32 ? ~0u : (1u << n0) - 1u, k1 = n1 == 32 ? ~0u : (1u << n1) - 1u;
@@ -553,7 +559,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
 #if PBR_BAL_PROFILE
     int iters = 0;
 #endif
-#if PBR_BAL_EXPERIMENT == 1  // timing experiment: no pass 2
+#if PBR_BAL_EXPERIMENT & 1  // timing experiment: no pass 2
     m = 0;
     if (!second) next_pixel();
     m = 0;

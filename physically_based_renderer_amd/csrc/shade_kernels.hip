@@ -498,6 +498,9 @@ __device__ __forceinline__ float reinhard_faithful(float c) { return c * __built
 template <int AMBIENT>
 __device__ __forceinline__ f3 ambient_term(const PixelInvariants& p, const PassArgs& ps, const float4* __restrict__ env) {
     const PixelInvariants& q = p;
+#if PBR_BAL_EXPERIMENT & 4  // development timing: no IBL block
+    if (AMBIENT == kAmbientIblDiffuse) return mk3(p.albedo.x * 0.5f, p.albedo.y * 0.5f, p.albedo.z * 0.5f);
+#endif
     if (AMBIENT == kAmbientIblDiffuse) {
         // Default.hlsl:141-146: kS = FresnelSchlick(N, V, F0); kD = (1 - kS)(1 - metallic);
         // irradiance = env.Sample(linear-wrap, WorldToSkyUV(N)); ambient = kD * (irradiance * albedo)
@@ -535,6 +538,9 @@ __device__ __forceinline__ float4 finish_lit(f3 ambient, float ao, f3 direct, co
 template <int AMBIENT, bool APPLY_AO>
 __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float ao, f3 direct, const PassArgs& ps,
                                                const float4* __restrict__ env, bool fast, bool faithful = false) {
+#if PBR_BAL_EXPERIMENT & 8  // development timing: no finish in faithful waves
+    if (faithful) return make_float4(direct.x, direct.y, direct.z, 1.0f);
+#endif
     return finish_lit<APPLY_AO>(ambient_term<AMBIENT>(p, ps, env), ao, direct, ps, fast, faithful);
 }
 

@@ -11,6 +11,7 @@ generates exactly its own rows and the gathered image is bit-identical to a sing
 """
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
@@ -52,17 +53,35 @@ def all_bands(height: int, world: int, align: int = 8) -> List[Band]:
     return [band_rows(height, world, r, align) for r in range(world)]
 
 
-def init_from_env(backend: str, always: bool = False) -> Tuple[int, int, int]:
+# Failure detection (the reference polls GetDeviceRemovedReason around every Draw step,
+# PBRApp.cpp:247): every collective of the process group -- the band gather included -- gives up after this many
+# seconds instead of blocking on a dead peer until the backend's default (30 min). RCCL's watchdog then aborts
+# the communicator and the process exits non-zero; gloo raises, and BandGather.wait turns that into GatherError.
+DEFAULT_TIMEOUT_S = 300.0
+
+
+class GatherError(RuntimeError):
+    """A band gather (or another collective) failed: a peer died, or it did not answer within the timeout."""
+
+
+def collective_timeout() -> datetime.timedelta:
+    """The process group's collective timeout: PBR_DIST_TIMEOUT_S seconds (default DEFAULT_TIMEOUT_S)."""
+    return datetime.timedelta(seconds=float(os.environ.get("PBR_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S)))
+
+
+def init_from_env(backend: str, always: bool = False, timeout: Optional[datetime.timedelta] = None
+                  ) -> Tuple[int, int, int]:
     """(rank, world, local_rank) from torchrun's environment; initialises the default group once: at
     world > 1, and at world 1 too when ``always`` (so a single-rank run exercises the same RCCL
-    communicator init / teardown and collectives as the multi-GPU one)."""
+    communicator init / teardown and collectives as the multi-GPU one). ``timeout`` (default
+    collective_timeout()) bounds every collective: a dead peer ends the run with an error, not a hang."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if (world > 1 or always) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        kwargs = {}
+        kwargs = {"timeout": timeout if timeout is not None else collective_timeout()}
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", local)  # one GPU per rank (RCCL)
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
@@ -111,17 +130,25 @@ class BandGather:
             self.frame[0].copy_(band_out)
             bufs = [torch.empty(tuple(band_out.shape), dtype=band_out.dtype) for _ in range(1, b.world)]
             works = [dist.irecv(buf, r, self.group) for r, buf in zip(range(1, b.world), bufs)]
-            for w in works:
-                w.wait()
+            BandGather.wait(works)
             for r, buf in zip(range(1, b.world), bufs):
                 self.frame[r].copy_(buf)
         else:
-            dist.send(band_out.cpu(), 0, self.group)
+            try:
+                dist.send(band_out.cpu(), 0, self.group)
+            except RuntimeError as e:
+                raise GatherError(f"rank {b.rank}: sending its band to rank 0 failed: {e}") from e
 
     @staticmethod
     def wait(handles) -> None:
+        """Wait for posted gather work; a failure (a dead peer, or no answer within the process group's
+        timeout) raises GatherError naming it."""
         for h in handles:
-            h.wait()
+            try:
+                h.wait()
+            except RuntimeError as e:
+                raise GatherError(f"band gather failed (peer lost or timed out; PBR_DIST_TIMEOUT_S="
+                                  f"{collective_timeout().total_seconds():g}): {e}") from e
 
     def assembled(self, height: int) -> Optional[torch.Tensor]:
         """Rank 0: the (height, W, 4) image stitched from the gathered slots (a copy when bands are

@@ -127,3 +127,80 @@ def test_cpu_baseline_rgba8_and_gathered_parity():
 def test_host_cpu_budget_reads_the_quota():
     b = bench.host_cpu_budget()
     assert b["used"] >= 1 and b["affinity"] >= b["used"]
+
+
+def test_bench_refuses_to_publish_a_wrong_frame(capsys):
+    """The north-star bar is enforced, not just reported: a bench line whose frame check misses 1e-5 relative (or
+    whose NaN pattern differs, or an RGBA8 code off by more than 1, or a failed gather checksum) is not printed on
+    stdout and main() exits with EXIT_PARITY -- the driver then records a failed run, never a throughput."""
+    from oracle import oracle as O
+
+    cfg = S.CONFIGS[3].with_size(128, 8)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    env = S.env_map()
+    frame = O.shade(list(planes), bench.oracle_pass_of(pc), pc.light_array(), env, n_threads=4)
+    base = {"metric": bench.METRIC, "value": 1.0}
+
+    def run(gpu_frame):
+        _, parity, _ = bench.cpu_baseline(cfg, planes, pc, env, gpu_frame, 0, "port")
+        rc = bench.emit_line({**base, **parity})
+        return rc, capsys.readouterr()
+
+    rc, out = run(frame)
+    assert rc == 0 and json.loads(out.out)["parity_ok"] is True
+    ok_within = frame.copy()
+    ok_within[3, 7, 1] *= 1 + 5e-6  # inside the bar
+    rc, out = run(ok_within)
+    assert rc == 0 and json.loads(out.out)["parity_ok"] is True
+    for breach in ("rel", "nan", "lost_nan"):
+        bad = frame.copy()
+        if breach == "rel":
+            bad[3, 7, 1] *= 1 + 2e-5
+        elif breach == "nan":
+            bad[0, 0, 0] = np.nan
+        else:
+            bad = bad[..., :3] * 0 + np.nan  # NaN everywhere the reference has numbers
+            bad = np.concatenate([bad, frame[..., 3:]], axis=-1).astype(np.float32)
+        rc, out = run(bad)
+        assert rc == bench.EXIT_PARITY, breach
+        assert out.out == "" and "PARITY FAILURE" in out.err
+    # the other checks a line can carry
+    for line in ({"parity_max_code_diff": 2}, {"gathered_frame_parity": {"parity_max_rel": 3e-5}},
+                 {"parity_max_rel": 0.0, "exact_mode": {"parity_max_rel": float("inf")}},
+                 {"gathered_frame_parity": {"parity_max_code_diff": 1}, "gather_checksums_match": False}):
+        assert bench.parity_failures(line), line
+        assert bench.emit_line({**base, **line}) == bench.EXIT_PARITY
+        assert capsys.readouterr().out == ""
+    assert bench.parity_failures({"parity_max_code_diff": 1, "gathered_frame_parity": {"parity_max_rel": 1e-5}}) == []
+    # a line without any check (--no-cpu-baseline) is printed and says so
+    assert bench.emit_line(dict(base)) == 0
+    assert json.loads(capsys.readouterr().out)["parity_checked"] is False
+
+
+def test_scale_anchor_ramps_the_clock_before_timing(monkeypatch):
+    """band_anchor runs the same untimed clock ramp as the headline (--ramp-ms) before its warm-up and timed
+    steps, and reports it; the anchor is then comparable with the ramped per-N values it divides."""
+    import argparse
+    import types
+
+    calls = []
+    monkeypatch.setattr(bench.torch.cuda, "synchronize", lambda *a, **k: None)
+
+    class Ctx:
+        def shade_frame(self, gb, o, fmt=None, stream=None):
+            calls.append("shade")
+
+    def fake_steps(shade_into, outs, stream, warmup, steps, *a, **k):
+        calls.append("timed")
+        return 0.01, [1.0] * steps
+
+    monkeypatch.setattr(bench, "shade_steps", fake_steps)
+    args = argparse.Namespace(rows_per_rank=8, mode="faithful", warmup=1, steps=4, ramp_ms=5.0)
+    resident = (types.SimpleNamespace(), [object(), object()])
+    a = bench.band_anchor(Ctx(), args, 1, None, None, resident)
+    assert a["clock_ramp"]["launches"] >= 8 and a["clock_ramp"]["ms"] >= 5.0
+    assert calls.index("timed") == len(calls) - 1 and calls[:-1] == ["shade"] * a["clock_ramp"]["launches"]
+    calls.clear()
+    a = bench.band_anchor(Ctx(), argparse.Namespace(**{**vars(args), "ramp_ms": 0.0}), 1, None, None, resident)
+    assert a["clock_ramp"] == {"ms": 0.0, "launches": 0} and calls == ["timed"]

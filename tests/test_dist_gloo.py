@@ -78,3 +78,48 @@ def test_row_bands_gather_equals_single_frame(world, height):
     whole = _oracle_band(cfg, D.band_rows(height, 1, 0), S.scene_pass(cfg), S.env_map())
     assert frame.shape == whole.shape
     assert np.array_equal(frame.view(np.uint32), whole.view(np.uint32))
+
+
+def _dead_peer_worker(rank, world, port, q, how):
+    """Rank 1 joins the group and then dies (or hangs) before it sends its band; rank 0's gather must give up with
+    GatherError -- at once for a lost connection, within the process group's timeout (PBR_DIST_TIMEOUT_S, here
+    4 s) for a silent peer -- not block."""
+    import sys
+    import time
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), PBR_DIST_TIMEOUT_S="4")
+    from physically_based_renderer_amd import dist as D
+
+    D.init_from_env("gloo")
+    band = D.band_rows(16, world, rank)
+    g = D.BandGather(band, 8, "cpu")
+    if rank == 1:
+        if how == "hangs":
+            time.sleep(12)
+        os._exit(17)  # a peer lost mid-run
+    t0 = time.perf_counter()
+    try:
+        D.BandGather.wait(g.start(torch.zeros((band.rows_max, 8, 4))))
+        q.put(("no error", time.perf_counter() - t0))
+    except D.GatherError as e:
+        q.put(("GatherError", time.perf_counter() - t0, str(e)))
+    os._exit(0)
+
+
+@pytest.mark.parametrize("how", ["dies", "hangs"])
+def test_gather_times_out_cleanly_when_a_peer_dies(how):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q, how)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert procs[1].exitcode == 17
+    assert res[0] == "GatherError", res
+    assert "PBR_DIST_TIMEOUT_S=4" in res[2]
+    assert res[1] < (15 if how == "hangs" else 60)  # the silent peer: the 4 s timeout, well before it wakes up

@@ -172,6 +172,7 @@ def test_bench_default_line_carries_anchor_and_executed_roofline(gpu):
     a = d["scale_anchor"]
     assert a["workload"] == "cfg5_8192x8192_64pt_ibl_rowbands_band64" or a["workload"].endswith("_band64")
     assert a["px_per_step"] == 8192 * 64 and a["output"] == "rgba8" and a["value"] > 0 and a["shade_ms"] > 0
+    assert a["clock_ramp"] == {"ms": 0.0, "launches": 0}  # --ramp-ms 0: the anchor ramps like the headline
     rf = d["roofline"]
     assert rf["bound"] == "mfma" and rf["flop_per_px"] == 5958
     st = rf["pass_stats"]
@@ -180,3 +181,21 @@ def test_bench_default_line_carries_anchor_and_executed_roofline(gpu):
     assert 0.3 * 64 * 3840 * 2160 < st["light_terms"] < 0.7 * 64 * 3840 * 2160
     assert rf["executed_flop_per_px"] < rf["flop_per_px"] and 0 < rf["frac_executed"] < rf["frac"]
     assert rf["pmc"]["kernel_sources_sha"] and (rf["traffic"] is None) == bool(rf["pmc"].get("stale"))
+
+
+def test_bench_exits_nonzero_on_a_parity_breach(gpu):
+    """The real bench process refuses a frame off the 1e-5 bar: with one channel of the checked frame scaled by
+    1 + 2e-5 it exits with bench.EXIT_PARITY and prints no metric line; the same run without the injection
+    prints its line with parity_ok true."""
+    import bench
+
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", "1", "--steps", "3",
+            "--warmup", "1", "--ramp-ms", "0", "--no-anchor", "--cpu-kind", "port"]
+    r = subprocess.run(base + ["--inject-parity-breach", "2e-5"], capture_output=True, text=True, timeout=600,
+                       cwd=ROOT)
+    assert r.returncode == bench.EXIT_PARITY, r.stderr[-3000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")] and "PARITY FAILURE" in r.stderr
+    r = subprocess.run(base, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["parity_ok"] is True and d["parity_checked"] is True and d["parity_max_rel"] <= 1e-5

@@ -57,6 +57,28 @@ def test_faithful_config_within_tolerance(cid, size, row_step, active, shading_c
     assert O.rel_err(exact[::row_step], ref).max() <= REL_TOL
 
 
+@pytest.mark.parametrize("cid", [3, 4])
+def test_full_frame_faithful_parity(cid, shading_ctx, gpu):
+    """The benchmark's mode over EVERY row of the full 3840x2160 frame -- config 3 (64 point lights + IBL,
+    wave-balanced faithful lists: the headline kernel) and config 4 (256 lights, tiled culling, F0 plane) --
+    against the oracle on 16 host threads: max relative error <= 1e-5 per channel, NaN exactly where the oracle
+    has NaN. bench.py refuses to print a throughput for a frame that misses this bar (parity_failures)."""
+    cfg = S.CONFIGS[cid]
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = with_flags(S.scene_pass(cfg), N.PBR_FLAG_FAITHFUL)
+    env = S.env_map() if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
+    gb = GBuffer.from_host(planes, gpu)
+    got = shade(shading_ctx, gb, pc, env)
+    del gb
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), env, n_threads=16)
+    assert got.shape == ref.shape == (cfg.height, cfg.width, 4)
+    e = O.rel_err(got, ref)
+    print(f"{cfg.name} full frame, faithful mode: max_rel={e.max():.3g} "
+          f"bit-identical {O.bit_equal(got, ref).mean():.4f}")
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert e.max() <= REL_TOL
+
+
 @pytest.mark.parametrize("name", golden_names())
 def test_faithful_golden_vectors(name, shading_ctx, gpu, env_map):
     """The golden fixtures (edge pixels with NaN/inf/subnormals/|N| > 1 included): waves outside the

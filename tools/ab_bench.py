@@ -56,7 +56,7 @@ def one(lib: str, cid: int, reps: int, flags: int = 0) -> dict:
         ms = [a.elapsed_time(b) for a, b in ev]
         bits = out.view(torch.int32).to(torch.int64)
         csum = int((bits * (torch.arange(bits.numel(), device=dev, dtype=torch.int64).view(bits.shape) % 65521 + 1)).sum())
-    return {"lib": os.path.basename(label), "config": cid, "median_ms": float(np.median(ms)), "min_ms": float(np.min(ms)),
+    return {"lib": label, "config": cid, "median_ms": float(np.median(ms)), "min_ms": float(np.min(ms)),
             "mpix_s": cfg.width * cfg.height / float(np.median(ms)) / 1e3, "checksum": csum}
 
 
@@ -95,7 +95,7 @@ def main():
             med = ms[len(ms) // 2]
             base = base or med
             same = all(x["checksum"] == ref_sum for x in results[(cid, lib)])
-            print(f"  cfg{cid} {os.path.basename(lib):28s} {med:.4f} ms  ({base / med:.4f}x vs first)  "
+            print(f"  cfg{cid} {lib:28s} {med:.4f} ms  ({base / med:.4f}x vs first)  "
                   f"frame {'==' if same else '!='} first lib's")
 
 
