@@ -520,6 +520,7 @@ def main():
 
     # The executed work of the last timed pass (pbr_last_pass_stats; every timed pass shades the same input).
     stats = ctx.pass_stats(stream)
+    kernel_name = ctx.last_kernel(stream)
     cull_note = {}
     if pc.flags & N.PBR_FLAG_TILED_CULLING:
         cull_note = {"lights_per_tile": round(stats["cull_tile_lights"] / max(stats["cull_tiles"], 1), 3),
@@ -583,7 +584,8 @@ def main():
         tflops_exec = fpp_exec * band_px / avg_kernel_s / 1e12
         # At 64 lights the arithmetic intensity (fpp / bpp ~ 99 FLOP/B) is 5x the ridge point, so the
         # FP32 vector (VALU) roof bounds the kernel: 157.3 TF (MI355X_MICROARCH.md). There is no matrix op
-        # on this path; "mfma" is the contract's name for the compute roof. HBM is reported beside it.
+        # on this path; "mfma" is the contract's name for the compute roof, and "compute_unit" says which unit
+        # that roof is: the VALU. HBM is reported beside it.
         compute_bound = fpp / bpp > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
         hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                "frac": round(achieved / HBM_PEAK_GBPS, 5)}
@@ -594,7 +596,8 @@ def main():
             "unit": "TFLOP/s" if compute_bound else "GB/s",
             "frac": round(tflops / FP32_PEAK_TFLOPS, 4) if compute_bound else hbm["frac"],
             "traffic": traffic,
-            "kernel": "shade_tile_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 4),
+            "compute_unit": "valu (fp32 vector ALU; no MFMA on this path)" if compute_bound else None,
+            "kernel": kernel_name, "avg_launch_ms": round(avg_kernel_s * 1e3, 4),
             "median_launch_ms": round(median_kernel_ms, 4),
             "flop_per_px": fpp, "bytes_per_px": bpp, "px_per_launch": band_px,
             "executed_flop_per_px": fpp_exec,
@@ -606,10 +609,11 @@ def main():
             "valu_issue_busy": valu_busy,
             "pmc": pmc_prov,
             "note": ("compute roof = the FP32 vector ALU (VALU, 157.3 TF packed; no matrix op on this path; 'mfma' is "
-                     "the contract's name for the compute roof); achieved / frac count SURVEY 8(d)'s algorithmic "
-                     "FLOPs (every light for every pixel); achieved_executed / frac_executed count only the terms "
-                     "the kernel evaluated (pass_stats: back-facing terms skipped by the wave-balanced lists and "
-                     "culled lights are not credited; the lists' back-face tests are); traffic = rocprofv3 "
+                     "the contract's name for the compute roof); frac / achieved count SURVEY 8(d)'s algorithmic-model "
+                     "FLOPs (every light for every pixel, which the kernel does not all evaluate); frac_executed / "
+                     "achieved_executed are the utilisation figure: only the terms the kernel evaluated (pass_stats: "
+                     "back-facing terms skipped by the wave-balanced lists and culled lights are not credited; the "
+                     "lists' back-face tests are); kernel = pbr_last_pass_kernel; traffic = rocprofv3 "
                      "FETCH_SIZE x2 + WRITE_SIZE bytes per launch and valu_issue_busy = SQ_ACTIVE_INST_VALU over "
                      "kernel cycles, from profiles/pmc_summary.json, quoted only when its kernel_sources_sha "
                      "equals this build's (pmc)"),
@@ -618,9 +622,11 @@ def main():
         parity = {}
         exact_leg = None
         frame = outs[0][: band.rows].cpu().numpy() if world == 1 else None  # the timed mode's frame
-        if frame is not None and args.inject_parity_breach:
+        if frame is not None and args.inject_parity_breach:  # test only: the largest channel, scaled
             frame = frame.copy()
-            frame.reshape(-1)[1] = frame.reshape(-1)[1] * (1.0 + args.inject_parity_breach) if not rgba8 else 255
+            flat = frame.reshape(-1)
+            k = int(np.argmax(np.where(np.isfinite(flat), np.abs(flat.astype(np.float64)), 0.0)))
+            flat[k] = flat[k] * (1.0 + args.inject_parity_breach) if not rgba8 else (int(flat[k]) + 2) % 256
         exact_frame = None
         assembled = gather.assembled(cfg.height).cpu().numpy() if world > 1 and gather is not None else None
         # The scaling anchor runs right after the timed steps, on a warm GPU, before the host-side legs (the CPU

@@ -18,7 +18,10 @@
  *     pbr_set_pass before it and waits (stream-side) for that upload when it was made on another
  *     stream, and a slot or texture is overwritten only after the queued passes that read it, on
  *     whatever stream they run. Host calls on one context are serialised by its mutex; the host
- *     order of pbr_set_pass and pbr_shade_* calls decides which pass a shade uses.
+ *     order of pbr_set_pass and pbr_shade_* calls decides which pass a shade uses. Contexts expect a
+ *     small, long-lived set of streams: the first call on a new stream synchronises the device once,
+ *     and past 16 streams the context forgets all but its last one then. Let a stream's passes
+ *     finish before destroying it (a new stream may reuse its handle value).
  * Plain C types only (hipStream_t is passed as void*).
  */
 #ifndef PBR_SHADE_H
@@ -30,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBR_ABI_VERSION 6
+#define PBR_ABI_VERSION 7
 #define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
 
 typedef enum pbr_status {
@@ -215,6 +218,12 @@ typedef struct pbr_pass_stats {
  * reported, and `stream` must then be ordered after that pass. All zero before the first pass.
  * The kernel writes one record per wave (workgroup in the one-pixel layout); this call sums them. */
 int pbr_last_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream);
+
+/* ABI 7: the kernel the last pass on `stream` launched (the same fallback as pbr_last_pass_stats), as the
+ * profiler names it without its argument list, e.g. "shade_tile_kernel<1, false, false, false, 1>"
+ * (the wave-balanced faithful lists) or "shade_lean_kernel<0, true, false, true, true>"; "" before the first
+ * pass. The string is owned by the context and stays valid until the next pass on that stream. */
+const char* pbr_last_pass_kernel(pbr_context* ctx, void* stream);
 
 /* ---- Host G-buffer fill (replaces the VS + rasteriser front-end, Default.hlsl:22-45) ---------- */
 

@@ -170,6 +170,7 @@ SIGNATURES = {
     "pbr_last_cull_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "pbr_last_pass_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(PassStats), ctypes.c_void_p]),
+    "pbr_last_pass_kernel": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_void_p]),
     "pbr_gbuffer_fill": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,
                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int32]),
     "pbr_gbuffer_fill_coverage": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,

@@ -22,8 +22,9 @@
 // (non-negative terms).
 //
 // The back-face test (pass 1) for light j at p_j and pixel P (l = p_j - P, the reference's L before it is
-// normalised), four FMAs per pixel:
-//   skip  <=>  t1 = N.p_j - N.P + c |N|_1 B_j < 0     (c = 2^-18 = 64u, u = 2^-24; N.P once per pixel)
+// normalised), three FMAs per pixel and light (c |N|_1 B - N.P is formed once per pixel, with one rounding):
+//   skip  <=>  t1 = N.p_j - N.P + c |N|_1 B < 0     (c = 2^-18 = 64u, u = 2^-24; B = max_j B_j >= B_j: a larger
+//                                                   margin only skips less, and the proof below holds for it)
 // B_j = B0_j + (|p_j|_1 + Pmax) / 8 (times 1 + 2^-20), where B0_j >= |l| for every pixel of the wave (the
 // L1 distance from the light to the centre of the wave's position box plus the box's L1 half-extent, with
 // margins for their roundings) and Pmax is the wave's largest |P|_1; computed once per wave, one lane per
@@ -102,10 +103,7 @@ constexpr int kBalRecX = 6;        // float4 per exchanged pixel record, exact p
 struct BalancedWaveLds {
     float4 rec[64 * kBalRec];  // 7 KiB
     union {
-        struct {
-            float4 bound[16];  // pass 1: the lights' distance bounds B_j (64 floats)
-            int hist[64];      // ranking
-        };
+        int hist[64];          // ranking
         int flag[128];         // pass 2 results: the pixel stayed inside the fast-path window, by origin
     };
     // By origin: exact passes, each pixel's sum before its point lights (written by the owner); then the
@@ -258,24 +256,25 @@ __device__ __forceinline__ float bal_wave_max(float v) {
     return v;
 }
 
-// Pass 1 for the pair and one light (position lx, ly, lz, bound bj): shift the light's SKIP bit for each pixel
-// (the sign of t1, see the header comment) into `ma` / `mb` (bit 31 after this call). nd = -N.P per pixel.
-__device__ __forceinline__ void push_skip_bits(uint32_t& ma, uint32_t& mb, float lx, float ly, float lz, float bj,
-                                               const f3x2& n, v2 nd, v2 cn) {
-    const v2 t1 = vfma(n.x, splat(lx), vfma(n.y, splat(ly), vfma(n.z, splat(lz), vfma(cn, splat(bj), nd))));
+// Pass 1 for the pair and one light (position lx, ly, lz): shift the light's SKIP bit for each pixel (the sign of
+// t1, see the header comment) into `ma` / `mb` (bit 31 after this call). kb = c |N|_1 B - N.P per pixel, with the
+// wave's bound B = max_j B_j (any B >= B_j keeps the skip proof: the margin term only grows), so the test is three
+// FMAs per pixel and light.
+__device__ __forceinline__ void push_skip_bits(uint32_t& ma, uint32_t& mb, float lx, float ly, float lz,
+                                               const f3x2& n, v2 kb) {
+    const v2 t1 = vfma(n.x, splat(lx), vfma(n.y, splat(ly), vfma(n.z, splat(lz), kb)));
     ma = __builtin_amdgcn_alignbit(ma, __float_as_uint(t1.x), 31);  // (m << 1) | sign(t1)
     mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(t1.y), 31);
 }
 
-// Pass 2's light records for one iteration (element 0: light j0; element 1: light j1 with the strength of
-// light s1) from the SoA staging: all twelve LDS reads issued back to back and one wait. Left to itself the
-// compiler interleaved reads and waits (three or four round trips per iteration), and the waves run this loop
-// nearly in step, so each round trip idled the SIMD.
-__device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0, int j1, int s1, f3x2& lp,
-                                                 f3x2& ls) {
+// Pass 2's light records for one iteration (element 0: light j0; element 1: light j1; index kBalMaxLights is the
+// zero sentinel: position and strength 0) from the SoA staging: all twelve LDS reads issued back to back and one
+// wait. Left to itself the compiler interleaved reads and waits (three or four round trips per iteration), and the
+// waves run this loop nearly in step, so each round trip idled the SIMD.
+__device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0, int j1, f3x2& lp, f3x2& ls) {
     typedef __attribute__((address_space(3))) const float lds_float;
     const uint32_t base = (uint32_t)(uintptr_t)(const lds_float*)lds_lights;
-    const uint32_t a0 = base + 4u * (uint32_t)j0, a1 = base + 4u * (uint32_t)j1, b1 = base + 4u * (uint32_t)s1;
+    const uint32_t a0 = base + 4u * (uint32_t)j0, a1 = base + 4u * (uint32_t)j1;
     float x0, x1, y0, y1, z0, z1, r0, r1, g0, g1, u0, u1;
     static_assert(kBalLdsStride * 4 == 272, "offsets below");
     asm volatile(
@@ -286,15 +285,15 @@ __device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0
         "ds_read_b32 %4, %12 offset:544\n\t"
         "ds_read_b32 %5, %13 offset:544\n\t"
         "ds_read_b32 %6, %12 offset:816\n\t"
-        "ds_read_b32 %7, %14 offset:816\n\t"
+        "ds_read_b32 %7, %13 offset:816\n\t"
         "ds_read_b32 %8, %12 offset:1088\n\t"
-        "ds_read_b32 %9, %14 offset:1088\n\t"
+        "ds_read_b32 %9, %13 offset:1088\n\t"
         "ds_read_b32 %10, %12 offset:1360\n\t"
-        "ds_read_b32 %11, %14 offset:1360\n\t"
+        "ds_read_b32 %11, %13 offset:1360\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(x0), "=&v"(x1), "=&v"(y0), "=&v"(y1), "=&v"(z0), "=&v"(z1), "=&v"(r0), "=&v"(r1), "=&v"(g0),
           "=&v"(g1), "=&v"(u0), "=&v"(u1)
-        : "v"(a0), "v"(a1), "v"(b1)
+        : "v"(a0), "v"(a1)
         : "memory");
     lp = f3x2{v2{x0, x1}, v2{y0, y1}, v2{z0, z1}};
     ls = f3x2{v2{r0, r1}, v2{g0, g1}, v2{u0, u1}};
@@ -306,7 +305,7 @@ __device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0
 // point_or_spot_faithful_x2<false, true, true> / brdf_faithful_x2<true, true> element for element (same
 // roundings, same window tests into `ok`).
 __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const f3x2& lp, const f3x2& ls, m2& ok,
-                                                      f3x2& sum) {
+                                                      f3x2& sum, uint64_t live) {
     f3x2 l = f3x2{lp.x - q.pos.x, lp.y - q.pos.y, lp.z - q.pos.z};
     const v2 dist = sqrt_nr(dot3(l, l));
     ok &= ge(dist, 0.01f);
@@ -320,7 +319,7 @@ __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const 
     const v2 den = inner * inner;
     const v2 n_dot_l = dot3_sat(n, l);
     const v2 r = rcp_hw((den * vfma(n_dot_l, splat(q.omk), splat(q.k))) * vfma(splat(q.nv), n_dot_l, splat(0.001f)));
-    const v2 p = pow5_faithful(1.0f - dot3_sat(h, splat3(q.v.x, q.v.y, q.v.z)));
+    const v2 p = pow5_faithful(1.0f - dot3_sat(h, splat3(q.v.x, q.v.y, q.v.z)), live);
     const f3x2 f = f3x2{q.f0.x + q.omf0.x * p, q.f0.y + q.omf0.y * p, q.f0.z + q.omf0.z * p};
     const v2 kr = (q.a2gv * n_dot_l) * r;
     const v2 w = att * n_dot_l;
@@ -389,17 +388,19 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
     const float slack = r + (fabsf(cx) + fabsf(cy) + fabsf(cz)) * 0x1p-22f;
     const float pmax = bal_wave_max(fmaxf(live_a ? (fabsf(pa.x) + fabsf(pa.y)) + fabsf(pa.z) : 0.0f,
                                           live_b ? (fabsf(pb.x) + fabsf(pb.y)) + fabsf(pb.z) : 0.0f));
-    if (lane_id < kBalLdsStride - 4) {  // B_j for j < n; padded lights (zero position) get a bound too
+    float bj = 0.0f;  // B_j of light j = lane (j < nl; padded lights: zero position, harmless), B = the maximum
+    if (lane_id < nl) {
         const float lx = lds_lights[lane_id], ly = lds_lights[kBalLdsStride + lane_id],
                     lz = lds_lights[2 * kBalLdsStride + lane_id];
         const float b0 = ((fabsf(lx - cx) + fabsf(ly - cy)) + fabsf(lz - cz)) + slack;
         const float far = ((fabsf(lx) + fabsf(ly)) + fabsf(lz)) + pmax;
-        reinterpret_cast<float*>(w.bound)[lane_id] = (b0 + 0.125f * far) * (1.0f + 0x1p-20f);
+        bj = (b0 + 0.125f * far) * (1.0f + 0x1p-20f);
     }
-    wave_lds_sync();
+    const float bmax = bal_wave_max(bj);
     const v2 cn = v2{0x1p-18f * ((fabsf(n.x.x) + fabsf(n.y.x)) + fabsf(n.z.x)),
                      0x1p-18f * ((fabsf(n.x.y) + fabsf(n.y.y)) + fabsf(n.z.y))};
     const v2 nd = -vfma(n.z, pos.z, vfma(n.y, pos.y, n.x * pos.x));  // -N.P
+    const v2 kb = vfma(cn, splat(bmax), nd);
     uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // skip bits; pixel a: a0 (lights 0..31), a1; pixel b: c0, c1
     // Four lights per step from uniform (broadcast) LDS reads, pushed from the highest light down so that
     // light j ends at bit j % 32 of its word. A word always runs all 32 of its lights (padded lights are zero
@@ -410,32 +411,29 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
     // waited on once (inline asm; left to itself the compiler waited after every few reads).
     typedef __attribute__((address_space(3))) const float lds_float;
     const uint32_t lbase = (uint32_t)(uintptr_t)(const lds_float*)lds_lights;
-    const uint32_t bbase = (uint32_t)(uintptr_t)(const lds_float*)reinterpret_cast<const float*>(w.bound);
     auto word = [&](int qbase, uint32_t& ma, uint32_t& mb) {  // lights [4 qbase, 4 qbase + 32)
         for (int k = 6; k >= 0; k -= 2) {  // steps k + 1 and k
-            const uint32_t la = lbase + 16u * (uint32_t)(qbase + k), ba = bbase + 16u * (uint32_t)(qbase + k);
-            float4 x1, y1, z1, b1, x0, y0, z0, b0;  // step k + 1 (lights 4(q + k) + 4..7), step k (+ 0..3)
+            const uint32_t la = lbase + 16u * (uint32_t)(qbase + k);
+            float4 x1, y1, z1, x0, y0, z0;  // step k + 1 (lights 4(q + k) + 4..7), step k (+ 0..3)
             asm volatile(
-                "ds_read_b128 %0, %8 offset:16\n\t"
-                "ds_read_b128 %1, %8 offset:288\n\t"
-                "ds_read_b128 %2, %8 offset:560\n\t"
-                "ds_read_b128 %3, %9 offset:16\n\t"
-                "ds_read_b128 %4, %8\n\t"
-                "ds_read_b128 %5, %8 offset:272\n\t"
-                "ds_read_b128 %6, %8 offset:544\n\t"
-                "ds_read_b128 %7, %9\n\t"
+                "ds_read_b128 %0, %6 offset:16\n\t"
+                "ds_read_b128 %1, %6 offset:288\n\t"
+                "ds_read_b128 %2, %6 offset:560\n\t"
+                "ds_read_b128 %3, %6\n\t"
+                "ds_read_b128 %4, %6 offset:272\n\t"
+                "ds_read_b128 %5, %6 offset:544\n\t"
                 "s_waitcnt lgkmcnt(0)"
-                : "=&v"(x1), "=&v"(y1), "=&v"(z1), "=&v"(b1), "=&v"(x0), "=&v"(y0), "=&v"(z0), "=&v"(b0)
-                : "v"(la), "v"(ba)
+                : "=&v"(x1), "=&v"(y1), "=&v"(z1), "=&v"(x0), "=&v"(y0), "=&v"(z0)
+                : "v"(la)
                 : "memory");
-            push_skip_bits(ma, mb, x1.w, y1.w, z1.w, b1.w, n, nd, cn);
-            push_skip_bits(ma, mb, x1.z, y1.z, z1.z, b1.z, n, nd, cn);
-            push_skip_bits(ma, mb, x1.y, y1.y, z1.y, b1.y, n, nd, cn);
-            push_skip_bits(ma, mb, x1.x, y1.x, z1.x, b1.x, n, nd, cn);
-            push_skip_bits(ma, mb, x0.w, y0.w, z0.w, b0.w, n, nd, cn);
-            push_skip_bits(ma, mb, x0.z, y0.z, z0.z, b0.z, n, nd, cn);
-            push_skip_bits(ma, mb, x0.y, y0.y, z0.y, b0.y, n, nd, cn);
-            push_skip_bits(ma, mb, x0.x, y0.x, z0.x, b0.x, n, nd, cn);
+            push_skip_bits(ma, mb, x1.w, y1.w, z1.w, n, kb);
+            push_skip_bits(ma, mb, x1.z, y1.z, z1.z, n, kb);
+            push_skip_bits(ma, mb, x1.y, y1.y, z1.y, n, kb);
+            push_skip_bits(ma, mb, x1.x, y1.x, z1.x, n, kb);
+            push_skip_bits(ma, mb, x0.w, y0.w, z0.w, n, kb);
+            push_skip_bits(ma, mb, x0.z, y0.z, z0.z, n, kb);
+            push_skip_bits(ma, mb, x0.y, y0.y, z0.y, n, kb);
+            push_skip_bits(ma, mb, x0.x, y0.x, z0.x, n, kb);
         }
     };
     const int n0 = nl < 32 ? nl : 32;
@@ -529,72 +527,95 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
 
     BAL_PROF_T(t2);
     // ---- pass 2
-    // Window results are per-lane bools here: the loop body runs under a partial exec mask, where a lane
-    // mask (m2, a ballot) has no bits for the inactive lanes -- ANDing it into a running mask would clear them.
-    // Faithful: two interleaved partial sums (acc); exact: one running sum per pixel (accx) in light order.
+    // Every lane runs every iteration (no divergent body): a lane with no live light left takes the zero sentinel
+    // (index kBalMaxLights: position and strength 0) for both elements, whose terms its dead accumulator absorbs.
+    // Lane state that is uniform in kind lives in scalar lane masks: `fail` (the lane's current pixel left the fast
+    // window for a live item; window tests are ballots, so only the bits of lanes with live items are ORed in),
+    // `second` (the lane is on its second pixel). Faithful: two interleaved partial sums (acc); exact: one running
+    // sum per pixel (accx) in light order.
     f3x2 acc = splat3(0.0f, 0.0f, 0.0f);
     f3 accx = mk3(0.0f, 0.0f, 0.0f);
-    bool ok = true;
-    bool second = false;
+    uint64_t fail = 0, second = 0;
     uint64_t m = ((uint64_t)cur.live1 << 32) | cur.live0;
-    // A finished pixel's result goes to LDS at once (its start slot, read already, and its flag), so that
-    // nothing of the first pixel stays in registers through the second one's iterations.
-    auto put_result = [&]() {
+    // A finished pixel's result goes to LDS at once (its start slot, read already, and its flag), so that nothing
+    // of it stays in registers: for the first pixel before the second one's iterations, for the second before the
+    // sentinel iterations that wait for the wave's other lanes.
+    auto put_result = [&]() {  // divergent: the lanes whose current pixel is done
         const f3 r = EXACT ? accx : mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
         w.start[0][cur.origin] = r.x;
         w.start[1][cur.origin] = r.y;
         w.start[2][cur.origin] = r.z;
-        w.flag[cur.origin] = ok ? 1 : 0;
+        w.flag[cur.origin] = on(fail) ? 0 : 1;
     };
     auto next_pixel = [&]() {  // divergent: the lanes whose first pixel is done
-        put_result();
         cur = load_item_any<EXACT>(&w.rec[R * lane_id]);
         m = ((uint64_t)cur.live1 << 32) | cur.live0;
         acc = splat3(0.0f, 0.0f, 0.0f);
         accx = mk3(0.0f, 0.0f, 0.0f);
-        ok = true;
-        second = true;
     };
-    if (m == 0) next_pixel();
+    // First pixels without a live light: hand them back and start the second ones at once (which may have none
+    // either: then they are handed back too, and those lanes run sentinels only).
+    {
+        const uint64_t done = lanes(m == 0);
+        if (done != 0) {  // uniform
+            if (on(done)) {
+                put_result();
+                next_pixel();
+            }
+            second = done;
+            const uint64_t empty = done & lanes(m == 0);
+            if (empty != 0 && on(empty)) put_result();
+        }
+    }
 #if PBR_BAL_PROFILE
     int iters = 0;
 #endif
 #if PBR_BAL_EXPERIMENT & 1  // timing experiment: no pass 2
-    m = 0;
-    if (!second) next_pixel();
+    if (on(~second)) {
+        put_result();
+        next_pixel();
+    }
+    second = ~0ull;
+    if (true) put_result();
     m = 0;
 #endif
     while (true) {
-        const bool active = m != 0;
-        if (__builtin_amdgcn_ballot_w64(active) == 0) break;
+        const uint64_t live = lanes(m != 0);
+        if (live == 0) break;
 #if PBR_BAL_PROFILE
         ++iters;
 #endif
-        if (active) {
-            const int j0 = __builtin_ctzll(m);
-            m &= m - 1;
-            // One light left: the second element's strength is the zero sentinel (index kBalMaxLights) and its
-            // position repeats the first element's light, so it adds +0 and passes the same window tests.
-            const int s1 = m != 0 ? __builtin_ctzll(m) : kBalMaxLights;
-            m &= m - 1;  // no-op when m == 0
-            const int j1 = s1 == kBalMaxLights ? j0 : s1;
-            m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests; only this lane's bits are read
-            f3x2 lp, ls;
-            read_pair_lights(lds_lights, j0, j1, s1, lp, ls);
-            if constexpr (EXACT) {
-                const f3x2 c = exact_point_items2(cur, lp, ls, oki);
-                accx = mk3((accx.x + c.x.x) + c.x.y, (accx.y + c.y.x) + c.y.y, (accx.z + c.z.x) + c.z.y);
-            } else {
-                faithful_point_items2(cur, lp, ls, oki, acc);
+        // Two live lights per lane (ctz saturating to the sentinel index: v_ffbl of 0 is -1), or the sentinel.
+        const int j0 = m != 0 ? __builtin_ctzll(m) : kBalMaxLights;
+        m &= m - 1;  // no-op when m == 0
+        const int j1 = m != 0 ? __builtin_ctzll(m) : kBalMaxLights;
+        m &= m - 1;
+        m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests, as lane masks
+        f3x2 lp, ls;
+        read_pair_lights(lds_lights, j0, j1, lp, ls);
+        if constexpr (EXACT) {
+            const f3x2 c = exact_point_items2(cur, lp, ls, oki);
+            accx = mk3((accx.x + c.x.x) + c.x.y, (accx.y + c.y.x) + c.y.y, (accx.z + c.z.x) + c.z.y);
+        } else {
+            faithful_point_items2(cur, lp, ls, oki, acc, live);
+        }
+        fail |= ~(oki.x & oki.y) & live;
+        // The lanes whose pixel just ran out of live lights.
+        const uint64_t done = lanes(m == 0) & live;
+        if (done != 0) {  // uniform
+            if (on(done)) {
+                put_result();
+                if (!on(second)) next_pixel();
             }
-            ok = ok && on(oki.x) && on(oki.y);
-            if (m == 0 && !second) next_pixel();
+            fail &= ~done;
+            const uint64_t first_done = done & ~second;
+            second |= first_done;
+            // A second pixel with no live light: hand it back now (rare).
+            const uint64_t empty = first_done & lanes(m == 0);
+            if (empty != 0 && on(empty)) put_result();
         }
     }
     BAL_PROF_T(t3);
-    // Every lane is on its second pixel now: a lane switches when its first pixel has no live light left,
-    // and the loop runs until no lane has one.
-    put_result();
     // ---- hand the results back: the owner reads its two pixels' (by origin 2 lane + element)
     wave_lds_sync();
     const float2 rx = reinterpret_cast<const float2*>(w.start[0])[lane_id];

@@ -36,6 +36,7 @@ struct StreamState {
     int64_t stats_capacity = 0;  // slots
     int64_t tiles = 0, slots = 0;
     bool culled = false;
+    std::string kernel;  // the last pass's kernel (pbr_last_pass_kernel)
 };
 
 struct Resource {
@@ -117,9 +118,17 @@ bool is_ambient_mode(int m) { return m == PBR_AMBIENT_CONSTANT || m == PBR_AMBIE
 
 void forget_readers(pbr_context* ctx);
 
+// Streams a context tracks at once. Contexts expect a small, long-lived set of streams (a FrameResource-style
+// ring); a caller that keeps creating new ones pays one device synchronisation per new stream, and past this
+// bound the table is pruned at that synchronisation, so it never grows without limit.
+constexpr size_t kMaxStreams = 16;
+
 // The StreamState of `s` (created on first use). Caller holds ctx->mu and the device guard. A new stream
 // beside existing ones: the device is synchronised once, so every pass queued so far is complete and no
-// resource has a pending reader (the single-stream passes recorded no event).
+// resource has a pending reader (the single-stream passes recorded no event). A full table is pruned then to the
+// context's last pass stream (whose statistics pbr_last_pass_stats falls back to): the others' records go, which
+// is safe as nothing of theirs is in flight. A destroyed stream whose handle value a new stream reuses is taken for
+// the old one; the contract (pbr_shade.h) asks callers to let a stream's passes finish before destroying it.
 int stream_index(pbr_context* ctx, hipStream_t s, hipError_t& e) {
     for (size_t i = 0; i < ctx->streams.size(); ++i)
         if (ctx->streams[i].stream == s) return (int)i;
@@ -127,6 +136,20 @@ int stream_index(pbr_context* ctx, hipStream_t s, hipError_t& e) {
         e = hipDeviceSynchronize();
         if (e != hipSuccess) return -1;
         forget_readers(ctx);
+        if (ctx->streams.size() >= kMaxStreams) {
+            std::vector<StreamState> keep;
+            for (size_t i = 0; i < ctx->streams.size(); ++i) {
+                StreamState& st = ctx->streams[i];
+                if ((int)i == ctx->last_stream) {
+                    keep.push_back(std::move(st));
+                    continue;
+                }
+                if (st.last_pass) (void)hipEventDestroy(st.last_pass);
+                if (st.d_stats) (void)hipFree(st.d_stats);
+            }
+            ctx->last_stream = keep.empty() ? -1 : 0;
+            ctx->streams = std::move(keep);
+        }
     }
     StreamState st;
     st.stream = s;
@@ -148,10 +171,11 @@ hipError_t before_write(pbr_context* ctx, Resource& r, hipStream_t w, int wi) {
     return hipSuccess;
 }
 
-// Wait on the host for every reader of `r` (before freeing its memory).
+// Wait on the host for every reader of `r` (before freeing its memory). The readers' streams are synchronised
+// themselves: a context used from one stream records no per-pass event, so an event wait would return at once.
 hipError_t before_free(pbr_context* ctx, Resource& r) {
     for (int i : r.readers) {
-        const hipError_t e = hipEventSynchronize(ctx->streams[i].last_pass);
+        const hipError_t e = hipStreamSynchronize(ctx->streams[i].stream);
         if (e != hipSuccess) return e;
     }
     r.readers.clear();
@@ -561,6 +585,7 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     if (e != hipSuccess) return fail_hip(ctx, e, "shade order");
     e = pbr::launch_shade(a, s);
     if (e != hipSuccess) return fail_hip(ctx, e, "shade_tile_kernel launch", PBR_ERR_LAUNCH);
+    st.kernel = pbr::launched_kernel(a);
     if (ctx->streams.size() > 1) {
         e = hipEventRecord(st.last_pass, s);
         if (e != hipSuccess) return fail_hip(ctx, e, "shade record");
@@ -660,6 +685,17 @@ int pbr_last_cull_stats(pbr_context* ctx, int64_t* sum_tile_lights, int64_t* num
 int pbr_last_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream) {
     if (!ctx || !out) return PBR_ERR_INVALID_ARGUMENT;
     return sum_pass_stats(ctx, out, stream, "pbr_last_pass_stats");
+}
+
+const char* pbr_last_pass_kernel(pbr_context* ctx, void* stream) {
+    if (!ctx) return "";
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int si = -1;
+    for (size_t i = 0; i < ctx->streams.size(); ++i)
+        if (ctx->streams[i].stream == s && ctx->streams[i].tiles > 0) si = (int)i;
+    if (si < 0) si = ctx->last_stream;
+    return si < 0 ? "" : ctx->streams[si].kernel.c_str();
 }
 
 }  // extern "C"

@@ -9,6 +9,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "libm_f32.h"
+#include "libm_f32_x2.h"
 
 namespace pbr {
 
@@ -96,20 +97,26 @@ __device__ __forceinline__ bool zero_or_in(float x, float lo, float hi) { return
 #if PBR_POW5_LDS
 __shared__ pbr_powf_log2_entry g_lds_powf_log2[16];
 __shared__ uint64_t g_lds_exp2f[32];
+__shared__ pbr_atan_seg g_lds_atan_seg[5];  // libm_f32_x2.h: atanf's reduction rows
+static __constant__ pbr_atan_seg pbr_atan_seg_tab[5] = PBR_ATAN_SEG_TABLE_INIT;
 // Every work-item of the block calls this, and a barrier follows before the first pow5.
 __device__ __forceinline__ void load_libm_tables() {
     const int t = threadIdx.x;
     if (t < 16) g_lds_powf_log2[t] = pbr_powf_log2_tab[t];
+    if (t >= 16 && t < 21) g_lds_atan_seg[t - 16] = pbr_atan_seg_tab[t - 16];
     if (t >= 32 && t < 64) g_lds_exp2f[t - 32] = pbr_exp2f_tab[t - 32];
 }
 #define PBR_POW5_TABLES g_lds_powf_log2, g_lds_exp2f
 #define PBR_LIBM_LOG2_TAB g_lds_powf_log2
 #define PBR_LIBM_EXP2_TAB g_lds_exp2f
+#define PBR_LIBM_ATAN_TAB g_lds_atan_seg
 #else
+static __constant__ pbr_atan_seg pbr_atan_seg_tab[5] = PBR_ATAN_SEG_TABLE_INIT;
 __device__ __forceinline__ void load_libm_tables() {}
 #define PBR_POW5_TABLES pbr_powf_log2_tab, pbr_exp2f_tab
 #define PBR_LIBM_LOG2_TAB pbr_powf_log2_tab
 #define PBR_LIBM_EXP2_TAB pbr_exp2f_tab
+#define PBR_LIBM_ATAN_TAB pbr_atan_seg_tab
 #endif
 #ifndef PBR_POW5_GLIBC_FROM  // x above which pow5_light switches to glibc's algorithm
 #define PBR_POW5_GLIBC_FROM 0.99f

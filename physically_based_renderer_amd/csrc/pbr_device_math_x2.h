@@ -316,14 +316,20 @@ constexpr float kInvPi = 0x1.45f306p-2f;  // RN(1/kPi)
 // so within 0.5 ulp + 2^-22 ulp of it and at most 1 ulp from glibc's powf (0.82 ulp), the same residue
 // the exact mode's fp64 x^5 has (pow5_light; DESIGN.md §2 counts it). 8 packed ops per pair instead of
 // 10 fp64 ones. The grazing band x > 0.99, where 1 - F cancels, keeps glibc's algorithm bit for bit.
-__device__ __forceinline__ v2 pow5_faithful(v2 x) {
+// `live`: the lanes whose result is used (the wave-balanced loop runs every lane, finished ones on zero-strength
+// sentinel items); the grazing branch is taken only for them.
+__device__ __forceinline__ v2 pow5_faithful(v2 x, uint64_t live = ~0ull) {
     const v2 x2 = x * x;
     const v2 e2 = vfma(x, x, -x2);
     const v2 x4 = x2 * x2;
     const v2 t = vfma(x2 + x2, e2, vfma(x2, x2, -x4));
     v2 p = vfma(x4, x, t * x);
-    if (__builtin_expect(x.x > PBR_POW5_GLIBC_FROM, 0)) p.x = pow5_glibc(x.x);
-    if (__builtin_expect(x.y > PBR_POW5_GLIBC_FROM, 0)) p.y = pow5_glibc(x.y);
+    if (__builtin_expect((lanes(x.x > PBR_POW5_GLIBC_FROM) & live) != 0, 0)) {
+        if (x.x > PBR_POW5_GLIBC_FROM && on(live)) p.x = pow5_glibc(x.x);
+    }
+    if (__builtin_expect((lanes(x.y > PBR_POW5_GLIBC_FROM) & live) != 0, 0)) {
+        if (x.y > PBR_POW5_GLIBC_FROM && on(live)) p.y = pow5_glibc(x.y);
+    }
     return p;
 }
 

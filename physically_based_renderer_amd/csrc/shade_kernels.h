@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 
 namespace pbr {
 
@@ -84,6 +85,8 @@ struct LaunchArgs {
 };
 
 hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream);
+// The kernel launch_shade launches for `a`, as rocprofv3 names it without the argument list.
+std::string launched_kernel(const LaunchArgs& a);
 // Number of tiles (workgroups) launch_shade uses for a width x height G-buffer.
 int64_t shade_tile_count(int width, int height, int pixels_per_thread);
 // Statistics records per tile: one per wave in the pair layout, one per workgroup in the one-pixel layout.

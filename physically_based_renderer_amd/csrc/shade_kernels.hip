@@ -519,6 +519,58 @@ __device__ __forceinline__ f3 ambient_term(const PixelInvariants& p, const PassA
     return mk3(ps.ambient[0] * p.albedo.x, ps.ambient[1] * p.albedo.y, ps.ambient[2] * p.albedo.z);
 }
 
+// The diffuse-IBL ambient of Default.hlsl:141-146 for both pixels of the pair in packed form: ambient_term's
+// operations element for element (FresnelSchlick(N, V) with kD = (1 - kS)(1 - metallic), WorldToSkyUV through the
+// branch-free pair forms of glibc's atan2f / asinf (libm_f32_x2.h, bit-identical), the linear-wrap env fetch per
+// pixel, kD * irradiance * albedo). Faithful waves take the IBL Fresnel x^5 from pow5_faithful (<= 1 ulp from glibc
+// off the grazing band x > 0.99, where it is glibc's: <= 1.2e-6 on kD); exact waves glibc's powf.
+// Pixels whose normal has a component the pair forms do not cover (NaN, inf, nonzero magnitudes outside
+// [2^-40, 2^40], |N.y| > 1) take the scalar functions. `live_a` / `live_b`: the elements whose result is used.
+__device__ __forceinline__ f3x2 ambient_ibl_pair(const PixelInvariants2& q, const PassArgs& ps,
+                                               const float4* __restrict__ env, bool faithful, bool live_a,
+                                               bool live_b) {
+    const v2 x = 1.0f - dot3_sat(q.n, q.v);  // 1 - saturate(dot(N, V)): the clamp bit maps NaN to 0 as hsat
+    const v2 pw = faithful ? pow5_faithful(x, lanes(live_a || live_b)) : v2{pow5_glibc(x.x), pow5_glibc(x.y)};
+    const f3x2 kd = f3x2{(1.0f - (q.f0.x + q.one_minus_f0.x * pw)) * q.one_minus_metal,
+                         (1.0f - (q.f0.y + q.one_minus_f0.y * pw)) * q.one_minus_metal,
+                         (1.0f - (q.f0.z + q.one_minus_f0.z * pw)) * q.one_minus_metal};
+    // WorldToSkyUV (LightingUtil.hlsl:216-225)
+    int sa[2], sb[2];
+    v2 ux = pbr_atan2f_x2(q.n.z, q.n.x, sa, PBR_LIBM_ATAN_TAB);
+    v2 uy = pbr_asinf_x2(q.n.y, sb);
+    const bool spec_a = live_a && (sa[0] | sb[0]), spec_b = live_b && (sa[1] | sb[1]);
+    if (__builtin_expect(lanes(spec_a || spec_b) != 0, 0)) {
+        if (spec_a) {
+            ux.x = pbr_atan2f(q.n.z.x, q.n.x.x);
+            uy.x = pbr_asinf(q.n.y.x);
+        }
+        if (spec_b) {
+            ux.y = pbr_atan2f(q.n.z.y, q.n.x.y);
+            uy.y = pbr_asinf(q.n.y.y);
+        }
+    }
+    ux = ux * 0.1591f;
+    uy = uy * 0.3183f;
+    ux = ux + 0.5f;
+    uy = uy + 0.5f;
+    uy = 1.0f - uy;
+    ux = 1.0f - ux;
+    ux = ux + 0.25f;
+    const f3 ia = sample_linear_wrap(env, ps.env_w, ps.env_h, ux.x, uy.x);
+    const f3 ib = sample_linear_wrap(env, ps.env_w, ps.env_h, ux.y, uy.y);
+    const f3x2 irr = f3x2{v2{ia.x, ib.x}, v2{ia.y, ib.y}, v2{ia.z, ib.z}};
+    return f3x2{kd.x * (irr.x * q.albedo.x), kd.y * (irr.y * q.albedo.y), kd.z * (irr.z * q.albedo.z)};
+}
+
+// The finish of both pixels of the pair (finish_pixel each): with the diffuse IBL, the ambient pair is formed in
+// packed form first (ambient_ibl_pair); `live_a` / `live_b` say which elements are shaded geometry.
+template <int AMBIENT, bool APPLY_AO>
+__device__ __forceinline__ void finish_pair(const PixelInvariants2& q2, const PixelInvariants& ua,
+                                            const PixelInvariants& ub, float ao_a, float ao_b, f3 da, f3 db,
+                                            const PassArgs& ps, const float4* __restrict__ env, bool fast_a,
+                                            bool fast_b, bool faithful, bool live_a, bool live_b, float4& ca,
+                                            float4& cb);
+
 // The rest of the PS from the ambient term: AO (extension), + direct, Reinhard, gamma (Default.hlsl:150-160).
 template <bool APPLY_AO>
 __device__ __forceinline__ float4 finish_lit(f3 ambient, float ao, f3 direct, const PassArgs& ps, bool fast,
@@ -533,6 +585,22 @@ __device__ __forceinline__ float4 finish_lit(f3 ambient, float ao, f3 direct, co
     lit = mk3(reinhard(lit.x, fast), reinhard(lit.y, fast), reinhard(lit.z, fast));  // Default.hlsl:153
     return make_float4(pow_inv_gamma(lit.x), pow_inv_gamma(lit.y), pow_inv_gamma(lit.z),
                        ps.opacity);
+}
+
+template <int AMBIENT, bool APPLY_AO>
+__device__ __forceinline__ void finish_pair(const PixelInvariants2& q2, const PixelInvariants& ua,
+                                            const PixelInvariants& ub, float ao_a, float ao_b, f3 da, f3 db,
+                                            const PassArgs& ps, const float4* __restrict__ env, bool fast_a,
+                                            bool fast_b, bool faithful, bool live_a, bool live_b, float4& ca,
+                                            float4& cb) {
+    if constexpr (AMBIENT == kAmbientIblDiffuse) {
+        const f3x2 amb = ambient_ibl_pair(q2, ps, env, faithful, live_a, live_b);
+        if (live_a) ca = finish_lit<APPLY_AO>(lane(amb, 0), ao_a, da, ps, fast_a, faithful);
+        if (live_b) cb = finish_lit<APPLY_AO>(lane(amb, 1), ao_b, db, ps, fast_b, faithful);
+    } else {
+        if (live_a) ca = finish_lit<APPLY_AO>(ambient_term<AMBIENT>(ua, ps, env), ao_a, da, ps, fast_a, faithful);
+        if (live_b) cb = finish_lit<APPLY_AO>(ambient_term<AMBIENT>(ub, ps, env), ao_b, db, ps, fast_b, faithful);
+    }
 }
 
 template <int AMBIENT, bool APPLY_AO>
@@ -978,12 +1046,11 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         }
     }
     float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca;
-    if (va)
-        ca = ga ? finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, da, ps, env, ok_a, faithful_wave)
-                : sky_pixel(ua.n, ps, fr.sky, !exact_only);
-    if (vb)
-        cb = gb_ ? finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, db, ps, env, ok_b, faithful_wave)
-                 : sky_pixel(ub.n, ps, fr.sky, !exact_only);
+    if (lanes(ga || gb_) != 0)  // wave-uniform
+        finish_pair<AMBIENT, APPLY_AO>(q2, ua, ub, ao_a, ao_b, da, db, ps, env, ok_a, ok_b, faithful_wave, ga, gb_, ca,
+                                       cb);
+    if (va && !ga) ca = sky_pixel(ua.n, ps, fr.sky, !exact_only);
+    if (vb && !gb_) cb = sky_pixel(ub.n, ps, fr.sky, !exact_only);
     bool keep_a, keep_b;
     alpha_keep_pair(gb, (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx, ga, gb_, ca,
                     cb, keep_a, keep_b);
@@ -1019,7 +1086,7 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
     const bool vb = (xa + 1 < gb.width) && (y < gb.height);
     const int geo_px = __popcll(lanes(va)) + __popcll(lanes(vb));
     if (geo_px == 0) {  // wholly outside the frame: nothing to shade, an empty statistics record
-        if ((tid & 63) == 0) {
+        if ((tid & 63) == 0 && tile_kept != nullptr) {
             int32_t* st = tile_kept + kStatsPerBlock * wave_global;
             for (int i = 0; i < kStatsPerBlock; ++i) st[i] = 0;
         }
@@ -1107,10 +1174,8 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
                 }
             }
             float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca;
-            if (va && !need_a)
-                ca = finish_pixel<AMBIENT, APPLY_AO>(ua, ao_a, lane(d2, 0), ps, env, ok_a, faithful_wave);
-            if (vb && !need_b)
-                cb = finish_pixel<AMBIENT, APPLY_AO>(ub, ao_b, lane(d2, 1), ps, env, ok_b, faithful_wave);
+            finish_pair<AMBIENT, APPLY_AO>(q2, ua, ub, ao_a, ao_b, lane(d2, 0), lane(d2, 1), ps, env, ok_a, ok_b,
+                                           faithful_wave, va && !need_a, vb && !need_b, ca, cb);
             bool keep_a, keep_b;
             alpha_keep_pair(gb, (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx,
                             va && !need_a, vb && !need_b, ca, cb, keep_a, keep_b);
@@ -1119,7 +1184,7 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         }
     }
     const int n_exact = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
-    if ((tid & 63) == 0) {
+    if ((tid & 63) == 0 && tile_kept != nullptr) {
         const bool culled = CULL;
         const int n_ps = culled ? kept_total : ps.n_point + ps.n_spot;
         int32_t* st = tile_kept + kStatsPerBlock * wave_global;
@@ -1440,6 +1505,17 @@ hipError_t launch_shade(const LaunchArgs& a, hipStream_t stream) {
     if (a.gb.width <= 0 || a.gb.height <= 0) return hipSuccess;
     return a.ambient_mode == kAmbientIblDiffuse ? dispatch_f0<kAmbientIblDiffuse>(a, stream)
                                                 : dispatch_f0<kAmbientConstant>(a, stream);
+}
+
+std::string launched_kernel(const LaunchArgs& a) {
+    if (a.gb.width <= 0 || a.gb.height <= 0) return "";
+    auto b = [](bool v) { return v ? std::string("true") : std::string("false"); };
+    const std::string t = std::to_string(a.ambient_mode == kAmbientIblDiffuse ? 1 : 0) + ", " + b(a.f0_plane) + ", " +
+                          b(a.apply_ao) + ", " + b(a.cull);
+    if (a.pixels_per_thread != 2) return "shade_tile1_kernel<" + t + ">";
+    if (!a.cull && a.ps.balanced != 0) return "shade_tile_kernel<" + t + ", " + std::to_string(a.ps.balanced) + ">";
+    if (a.lean) return "shade_lean_kernel<" + t + ", " + b(a.ps.faithful != 0) + ">";
+    return "shade_tile_kernel<" + t + ", 0>";
 }
 
 int64_t shade_tile_count(int width, int height, int pixels_per_thread) {

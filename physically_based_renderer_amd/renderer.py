@@ -286,6 +286,12 @@ class ShadingContext:
                 "pbr_last_pass_stats", self._h)
         return {name: getattr(st, name) for name, _ in N.PassStats._fields_}
 
+    def last_kernel(self, stream=None) -> str:
+        """pbr_last_pass_kernel: the kernel the last pass on ``stream`` launched, as rocprofv3 names it without
+        its argument list ("" before the first pass)."""
+        fn = getattr(self.lib, "pbr_last_pass_kernel", None)  # absent only from older A/B builds (PBR_LIB_PATH)
+        return "" if fn is None else (fn(self._h, ctypes.c_void_p(_stream_handle(stream))) or b"").decode()
+
     def cull_stats(self, stream=None):
         """(sum of surviving point/spot lights over tiles, tiles) of the last pass ((0, 0) unless it culled)."""
         s, t = ctypes.c_int64(), ctypes.c_int64()

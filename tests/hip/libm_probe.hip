@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "libm_f32.h"
+#include "libm_f32_x2.h"
 
 namespace {
 
@@ -28,7 +29,11 @@ __host__ __device__ inline uint64_t mix(uint64_t z) {
 
 inline float bits_to_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 inline uint32_t float_bits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
-inline bool same(float a, float b) { return float_bits(a) == float_bits(b) || (a != a && b != b); }
+// Any NaN matches any NaN -- except the pair probes' "special element" marker, which must match exactly.
+inline bool same(float a, float b) {
+    if (float_bits(a) == 0x7fc0deadu || float_bits(b) == 0x7fc0deadu) return float_bits(a) == float_bits(b);
+    return float_bits(a) == float_bits(b) || (a != a && b != b);
+}
 
 // Pair i of the random atan2f set (host and device agree on it).
 __host__ __device__ inline void pair(uint64_t seed, uint64_t i, float& y, float& x) {
@@ -59,6 +64,38 @@ __global__ void k_pairs(uint64_t seed, uint64_t first, uint64_t n, float* out) {
     float y, x;
     pair(seed, first + i, y, x);
     out[i] = pbr_atan2f(y, x);
+}
+
+__constant__ pbr_atan_seg k_atan_tab[5] = PBR_ATAN_SEG_TABLE_INIT;
+
+// The pair forms (libm_f32_x2.h): work-item i evaluates inputs 2i and 2i + 1 together; a special element (the
+// caller's scalar fallback) is written as a NaN with payload 0x7fc0dead so the host can tell it apart.
+__global__ void k_unary_x2(int which, uint32_t base, uint64_t n, float* out) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (2 * i >= n) return;
+    const pbr_lv2 v = {__uint_as_float(base + (uint32_t)(2 * i)), __uint_as_float(base + (uint32_t)(2 * i + 1))};
+    int sp[2];
+    const pbr_lv2 r = which == 0 ? pbr_asinf_x2(v, sp) : pbr_atan2f_x2(v, (pbr_lv2)(1.0f), sp, k_atan_tab);
+    out[2 * i] = sp[0] ? __uint_as_float(0x7fc0deadu) : r.x;
+    if (2 * i + 1 < n) out[2 * i + 1] = sp[1] ? __uint_as_float(0x7fc0deadu) : r.y;
+}
+
+__global__ void k_pairs_x2(uint64_t seed, uint64_t first, uint64_t n, float* out) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (2 * i >= n) return;
+    float y0, x0, y1, x1;
+    pair(seed, first + 2 * i, y0, x0);
+    pair(seed, first + 2 * i + 1, y1, x1);
+    int sp[2];
+    const pbr_lv2 r = pbr_atan2f_x2((pbr_lv2){y0, y1}, (pbr_lv2){x0, x1}, sp, k_atan_tab);
+    out[2 * i] = sp[0] ? __uint_as_float(0x7fc0deadu) : r.x;
+    if (2 * i + 1 < n) out[2 * i + 1] = sp[1] ? __uint_as_float(0x7fc0deadu) : r.y;
+}
+
+// The inputs the pair forms must hand to the scalar functions.
+inline bool atan2_special(float y, float x) {
+    auto in = [](float v) { const float a = std::fabs(v); return a == 0.0f || (a >= 0x1p-40f && a <= 0x1p40f); };
+    return !(in(y) && in(x));
 }
 
 template <class F>
@@ -124,6 +161,56 @@ extern "C" long long probe_atan2_pairs(uint64_t seed, uint64_t n_total, float* b
         const uint64_t b = compare_parallel(n, h, [&](uint64_t i) {
             float y, x;
             pair(seed, first + i, y, x);
+            return atan2f(y, x);
+        }, &fi);
+        if (b && bad == 0) pair(seed, first + fi, *bad_y, *bad_x);
+        bad += (long long)b;
+    }
+    hipFree(d);
+    hipHostFree(h);
+    return bad;
+}
+
+// The pair forms, checked like the scalar ones: `which` 0 = pbr_asinf_x2, 1 = pbr_atan2f_x2(y, 1) over the bit
+// patterns [lo, hi]; an element they flag special must be exactly one the scalar function is needed for, every other
+// element must carry glibc's bits. Returns mismatches (either kind) or -1; *first_bad as probe_unary.
+extern "C" long long probe_unary_x2(int which, uint32_t lo, uint32_t hi, uint32_t* first_bad) {
+    float *d = nullptr, *h = nullptr;
+    if (hipMalloc(&d, kChunk * 4) != hipSuccess || hipHostMalloc(&h, kChunk * 4) != hipSuccess) return -1;
+    long long bad = 0;
+    *first_bad = 0xffffffffu;
+    for (uint64_t base = lo; base <= hi; base += kChunk) {
+        const uint64_t n = std::min<uint64_t>(kChunk, (uint64_t)hi - base + 1);
+        hipLaunchKernelGGL(k_unary_x2, dim3((unsigned)((n / 2 + 256) / 256)), dim3(256), 0, 0, which, (uint32_t)base, n, d);
+        if (hipMemcpy(h, d, n * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        uint64_t fi;
+        const uint64_t b = compare_parallel(n, h, [&](uint64_t i) -> float {
+            const float v = bits_to_float((uint32_t)(base + i));
+            const bool special = which == 0 ? (std::fabs(v) > 1.0f || v != v) : atan2_special(v, 1.0f);
+            if (special) return __builtin_bit_cast(float, 0x7fc0deadu);
+            return which == 0 ? asinf(v) : atan2f(v, 1.0f);
+        }, &fi);
+        if (b && *first_bad == 0xffffffffu) *first_bad = (uint32_t)(base + fi);
+        bad += (long long)b;
+    }
+    hipFree(d);
+    hipHostFree(h);
+    return bad;
+}
+
+extern "C" long long probe_atan2_pairs_x2(uint64_t seed, uint64_t n_total, float* bad_y, float* bad_x) {
+    float *d = nullptr, *h = nullptr;
+    if (hipMalloc(&d, kChunk * 4) != hipSuccess || hipHostMalloc(&h, kChunk * 4) != hipSuccess) return -1;
+    long long bad = 0;
+    for (uint64_t first = 0; first < n_total; first += kChunk) {
+        const uint64_t n = std::min<uint64_t>(kChunk, n_total - first);
+        hipLaunchKernelGGL(k_pairs_x2, dim3((unsigned)((n / 2 + 256) / 256)), dim3(256), 0, 0, seed, first, n, d);
+        if (hipMemcpy(h, d, n * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        uint64_t fi;
+        const uint64_t b = compare_parallel(n, h, [&](uint64_t i) -> float {
+            float y, x;
+            pair(seed, first + i, y, x);
+            if (atan2_special(y, x)) return __builtin_bit_cast(float, 0x7fc0deadu);
             return atan2f(y, x);
         }, &fi);
         if (b && bad == 0) pair(seed, first + fi, *bad_y, *bad_x);

@@ -94,6 +94,32 @@ def test_device_atan2f_pairs_equal_glibc(probes):
     assert bad == 0, f"{bad} mismatches, first atan2f({y.value!r}, {x.value!r})"
 
 
+@pytest.mark.parametrize("which,ranges", [(0, [(0, 0x3F800000 + 0x100000), (0x80000000, 0xBF800000 + 0x100000)]),
+                                          (1, [(0, 0x7F7FFFFF), (0x80000000, 0xFF7FFFFF)])])
+def test_device_libm_pair_forms_equal_glibc(probes, which, ranges):
+    """The branch-free pair forms (libm_f32_x2.h: pbr_asinf_x2 over every float in [-1, 1] and a stretch past it,
+    pbr_atan2f_x2(y, 1) over every finite y), evaluated on the device two arguments per work-item: glibc's bits
+    wherever they do not flag an element special, and flagged exactly where the scalar function is needed
+    (|x| > 1 / NaN; atan2f components outside 0 or [2^-40, 2^40])."""
+    L = probes["libm_probe"]
+    L.probe_unary_x2.restype = ctypes.c_longlong
+    L.probe_unary_x2.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    for lo, hi in ranges:
+        first = ctypes.c_uint32()
+        bad = L.probe_unary_x2(which, lo, hi, ctypes.byref(first))
+        assert bad == 0, f"{['asinf_x2', 'atan2f_x2(y,1)'][which]}: {bad} mismatches, first 0x{first.value:08x}"
+
+
+def test_device_atan2f_pair_form_random_pairs_equal_glibc(probes):
+    L = probes["libm_probe"]
+    L.probe_atan2_pairs_x2.restype = ctypes.c_longlong
+    L.probe_atan2_pairs_x2.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_float),
+                                       ctypes.POINTER(ctypes.c_float)]
+    y, x = ctypes.c_float(), ctypes.c_float()
+    bad = L.probe_atan2_pairs_x2(2025, 1 << 27, ctypes.byref(y), ctypes.byref(x))
+    assert bad == 0, f"{bad} mismatches, first atan2f({y.value!r}, {x.value!r})"
+
+
 def test_faithful_gamma_error_exhaustive(probes):
     """PBR_FLAG_FAITHFUL's gamma encode vs the host glibc powf(c, 1/2.2f) on every float of the binades
     [2^-14, 1): within 5.4e-7 relative (9 x 2^-24) where the hardware exp2/log2 path runs (c >= 2^-10),

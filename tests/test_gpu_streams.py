@@ -171,3 +171,53 @@ def test_geometry_pixels_follow_the_coverage_plane(gpu):
     assert 0 < geo < cfg.width * cfg.height
     assert st["geometry_pixels"] == geo
     assert st["light_terms"] == (pc.num_dir_lights + pc.num_point_lights + pc.num_spot_lights) * geo
+
+
+def test_many_short_lived_streams_stay_correct_and_bounded():
+    """A caller that creates a new stream per frame (40 of them, each destroyed after its frame completed): every
+    frame equals the pass shaded on the default stream, and the context's stream table stays bounded (it is pruned
+    at the device synchronisation a new stream costs; pbr_context.hip kMaxStreams) -- the frames after the pruning
+    still carry the right bits and statistics."""
+    cfg = S.CONFIGS[2].with_size(256, 64)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = S.scene_pass(cfg)
+    with ShadingContext(0) as ctx:
+        gb = GBuffer.from_host(planes, torch.device("cuda", 0))
+        ctx.set_pass(pc)
+        ref = ctx.shade(gb)
+        torch.cuda.synchronize()
+        ref_np, ref_stats = ref.cpu().numpy(), ctx.pass_stats()
+        for k in range(40):
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                if k % 3 == 0:
+                    ctx.set_pass(pc, s)  # a new light slot uploaded on the short-lived stream too
+                out = ctx.shade(gb, stream=s)
+                st = ctx.pass_stats(s)
+                s.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), ref_np.view(np.uint32)), k
+            assert st == ref_stats, k
+            del s
+
+
+def test_last_pass_kernel_names_the_launched_kernel():
+    """pbr_last_pass_kernel (ABI 7) names the kernel each kind of pass launches, as rocprofv3 does."""
+    dev = torch.device("cuda", 0)
+    with ShadingContext(0) as ctx:
+        assert ctx.last_kernel() == ""
+        for cid, flags, want in ((3, N.PBR_FLAG_FAITHFUL, "shade_tile_kernel<1, false, false, false, 1>"),
+                                 (3, 0, "shade_tile_kernel<1, false, false, false, 2>"),
+                                 (2, N.PBR_FLAG_FAITHFUL, "shade_lean_kernel<0, false, false, false, true>"),
+                                 (2, 0, "shade_lean_kernel<0, false, false, false, false>"),
+                                 (4, N.PBR_FLAG_FAITHFUL, "shade_lean_kernel<0, true, false, true, true>"),
+                                 (2, N.PBR_FLAG_EXACT_ONLY, "shade_tile_kernel<0, false, false, false, 0>")):
+            cfg = S.CONFIGS[cid].with_size(128, 16)
+            planes, _ = S.fill_gbuffer_host(cfg)
+            pc = S.scene_pass(cfg)
+            pc = _with(pc, flags=int(pc.flags) | flags)
+            ctx.set_pass(pc)
+            if pc.ambient_mode:
+                ctx.set_env_map(S.env_map())
+            ctx.shade(GBuffer.from_host(planes, dev))
+            torch.cuda.synchronize()
+            assert ctx.last_kernel() == want, (cid, flags)

@@ -154,6 +154,25 @@ def test_libm_port_matches_host_glibc(tmp_path):
     assert out.count("mismatches 0") == 7, out
 
 
+def test_libm_pair_forms_match_host_glibc(tmp_path):
+    """libm_f32_x2.h, the branch-free pair forms of atan2f / asinf the shading kernels' diffuse IBL runs, compiled
+    for the host: glibc's bits wherever they do not flag an element for the scalar function, and flagged exactly
+    where that is needed. tools/libm_x2_check.cpp without --quick is the exhaustive version (every float of
+    asinf's domain, every finite atan2f(y, 1), 2e9 random pairs: 0 mismatches), tests/test_gpu_probes.py the
+    device one."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "lx2")
+    subprocess.run(["/opt/rocm/llvm/bin/clang++", "-std=c++17", "-O2", "-ffp-contract=off", "-fno-builtin", "-I",
+                    os.path.join(root, "physically_based_renderer_amd", "csrc"),
+                    os.path.join(root, "tools", "libm_x2_check.cpp"), "-o", exe, "-lm", "-lpthread"], check=True)
+    r = subprocess.run([exe, "--quick"], capture_output=True, text=True)
+    print(r.stdout)
+    assert r.returncode == 0 and r.stdout.count(" 0 mismatches  0 special-flag errors") == 5, r.stdout
+
+
 def _rgbe_expected(rgbe):
     e = rgbe[..., 3].astype(np.int64)
     return np.where(e[..., None] > 0, rgbe[..., :3].astype(np.float64) * np.ldexp(1.0, e[..., None] - 136),
