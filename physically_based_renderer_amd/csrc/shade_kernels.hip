@@ -529,6 +529,9 @@ __device__ __forceinline__ f3 ambient_term(const PixelInvariants& p, const PassA
 __device__ __forceinline__ f3x2 ambient_ibl_pair(const PixelInvariants2& q, const PassArgs& ps,
                                                const float4* __restrict__ env, bool faithful, bool live_a,
                                                bool live_b) {
+#if PBR_BAL_EXPERIMENT & 4  // development timing: no IBL block
+    return f3x2{q.albedo.x * 0.5f, q.albedo.y * 0.5f, q.albedo.z * 0.5f};
+#endif
     const v2 x = 1.0f - dot3_sat(q.n, q.v);  // 1 - saturate(dot(N, V)): the clamp bit maps NaN to 0 as hsat
     const v2 pw = faithful ? pow5_faithful(x, lanes(live_a || live_b)) : v2{pow5_glibc(x.x), pow5_glibc(x.y)};
     const f3x2 kd = f3x2{(1.0f - (q.f0.x + q.one_minus_f0.x * pw)) * q.one_minus_metal,
@@ -536,8 +539,13 @@ __device__ __forceinline__ f3x2 ambient_ibl_pair(const PixelInvariants2& q, cons
                          (1.0f - (q.f0.z + q.one_minus_f0.z * pw)) * q.one_minus_metal};
     // WorldToSkyUV (LightingUtil.hlsl:216-225)
     int sa[2], sb[2];
+#if PBR_BAL_EXPERIMENT & 2  // development timing: no atan2f / asinf
+    v2 ux = q.n.z * 0.5f + q.n.x, uy = q.n.y * 0.5f;
+    sa[0] = sa[1] = sb[0] = sb[1] = 0;
+#else
     v2 ux = pbr_atan2f_x2(q.n.z, q.n.x, sa, PBR_LIBM_ATAN_TAB);
     v2 uy = pbr_asinf_x2(q.n.y, sb);
+#endif
     const bool spec_a = live_a && (sa[0] | sb[0]), spec_b = live_b && (sa[1] | sb[1]);
     if (__builtin_expect(lanes(spec_a || spec_b) != 0, 0)) {
         if (spec_a) {
