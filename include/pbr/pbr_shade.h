@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBR_ABI_VERSION 7
+#define PBR_ABI_VERSION 8
 #define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
 
 typedef enum pbr_status {
@@ -224,6 +224,16 @@ int pbr_last_pass_stats(pbr_context* ctx, pbr_pass_stats* out, void* stream);
  * (the wave-balanced faithful lists) or "shade_lean_kernel<0, true, false, true, true>"; "" before the first
  * pass. The string is owned by the context and stays valid until the next pass on that stream. */
 const char* pbr_last_pass_kernel(pbr_context* ctx, void* stream);
+
+/* ABI 8: the bounds-checked kernel build (PBR_DEBUG_BOUNDS=1: `make -C physically_based_renderer_amd/csrc
+ * debug-bounds`: physically_based_renderer_amd/_lib/debug_bounds/libpbrshade.so), the analogue of the reference's D3D12 debug layer
+ * (d3dApp.cpp:443-444). Its kernels check every G-buffer, output, coverage, texel and light index (and the
+ * wave-balanced lists' LDS indices) against the launch's extents; a violation is recorded, not trapped, and the
+ * access is redirected to index 0. Synchronises the context's device, then copies its flags into `flags`
+ * (16 words, may be NULL): flags[c] != 0 when index class c was violated (0 G-buffer, 1 output, 2 coverage,
+ * 3 texel, 4 light, 5 LDS list), flags[8 + c] the last offending index; `reset` != 0 clears them. Every pass since
+ * the first context on the device (or the last reset) counts. PBR_ERR_UNSUPPORTED from a product build. */
+int pbr_debug_bounds(pbr_context* ctx, uint32_t* flags, int reset);
 
 /* ---- Host G-buffer fill (replaces the VS + rasteriser front-end, Default.hlsl:22-45) ---------- */
 

@@ -16,6 +16,13 @@ HEADER_PATH = os.path.join(REPO_DIR, "include", "pbr", "pbr_shade.h")
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
 
 PBR_OK = 0
+PBR_ERR_INVALID_ARGUMENT = -1
+PBR_ERR_NO_DEVICE = -2
+PBR_ERR_OUT_OF_MEMORY = -3
+PBR_ERR_LAUNCH = -4
+PBR_ERR_HIP = -5
+PBR_ERR_NOT_READY = -6
+PBR_ERR_UNSUPPORTED = -7
 PBR_MAX_LIGHTS = 4096
 PBR_AMBIENT_CONSTANT = 0
 PBR_AMBIENT_IBL_DIFFUSE = 1
@@ -171,6 +178,7 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "pbr_last_pass_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(PassStats), ctypes.c_void_p]),
     "pbr_last_pass_kernel": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_void_p]),
+    "pbr_debug_bounds": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "pbr_gbuffer_fill": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,
                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int64, ctypes.c_int32]),
     "pbr_gbuffer_fill_coverage": (ctypes.c_int64, [ctypes.POINTER(SceneDesc), ctypes.c_int32, ctypes.c_int32,

@@ -273,6 +273,8 @@ __device__ __forceinline__ void push_skip_bits(uint32_t& ma, uint32_t& mb, float
 // waves run this loop nearly in step, so each round trip idled the SIMD.
 __device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0, int j1, f3x2& lp, f3x2& ls) {
     typedef __attribute__((address_space(3))) const float lds_float;
+    j0 = PBR_BOUNDS(j0, kBalMaxLights + 1, kBoundsLds);
+    j1 = PBR_BOUNDS(j1, kBalMaxLights + 1, kBoundsLds);
     const uint32_t base = (uint32_t)(uintptr_t)(const lds_float*)lds_lights;
     const uint32_t a0 = base + 4u * (uint32_t)j0, a1 = base + 4u * (uint32_t)j1;
     float x0, x1, y0, y1, z0, z1, r0, r1, g0, g1, u0, u1;
@@ -542,10 +544,11 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     // sentinel iterations that wait for the wave's other lanes.
     auto put_result = [&]() {  // divergent: the lanes whose current pixel is done
         const f3 r = EXACT ? accx : mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
-        w.start[0][cur.origin] = r.x;
-        w.start[1][cur.origin] = r.y;
-        w.start[2][cur.origin] = r.z;
-        w.flag[cur.origin] = on(fail) ? 0 : 1;
+        const int o = PBR_BOUNDS(cur.origin, 128, kBoundsLds);
+        w.start[0][o] = r.x;
+        w.start[1][o] = r.y;
+        w.start[2][o] = r.z;
+        w.flag[o] = on(fail) ? 0 : 1;
     };
     auto next_pixel = [&]() {  // divergent: the lanes whose first pixel is done
         cur = load_item_any<EXACT>(&w.rec[R * lane_id]);

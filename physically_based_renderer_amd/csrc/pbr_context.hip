@@ -13,6 +13,7 @@
 
 #include "pbr/pbr_shade.h"
 #include "shade_kernels.h"
+#include "pbr_debug_bounds.h"
 
 // Cross-stream ordering of the context's device resources (the reference's 3-deep FrameResource ring,
 // FrameResource.h:111-140, PBRApp.cpp:220-243, is the same idea on D3D12 fences). A resource -- a light slot,
@@ -117,6 +118,40 @@ int fail_hip(pbr_context* ctx, hipError_t e, const char* what, int status = PBR_
 bool is_ambient_mode(int m) { return m == PBR_AMBIENT_CONSTANT || m == PBR_AMBIENT_IBL_DIFFUSE; }
 
 void forget_readers(pbr_context* ctx);
+
+// PBR_DEBUG_BOUNDS builds (pbr_debug_bounds.h): one bounds-flag buffer per device, allocated, cleared and published
+// to the kernels by the first context created on it; product builds have none.
+constexpr int kBoundsMaxDevices = 64;
+constexpr size_t kBoundsBytes = sizeof(uint32_t) * 2 * pbr::kBoundsClasses;
+std::mutex g_bounds_mu;
+uint32_t* g_bounds_buf[kBoundsMaxDevices] = {};
+
+hipError_t arm_bounds(int dev) {  // current device = dev
+    if (!PBR_DEBUG_BOUNDS) return hipSuccess;
+    if (dev < 0 || dev >= kBoundsMaxDevices) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_bounds_mu);
+    if (g_bounds_buf[dev]) return hipSuccess;
+    uint32_t* b = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&b), kBoundsBytes);
+    if (e == hipSuccess) e = hipMemset(b, 0, kBoundsBytes);
+    if (e == hipSuccess) e = pbr::debug_bounds_publish(b);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess)
+        g_bounds_buf[dev] = b;
+    else if (b)
+        (void)hipFree(b);
+    return e;
+}
+
+// PBR_DEBUG_BOUNDS_SKEW=1 (bounds-checked builds): the output extent the checks use is one column narrower than
+// the frame, so every pass must report class 1 -- the negative control of tests/test_gpu_debug_bounds.py.
+bool debug_bounds_skew() {
+    static const bool skew = [] {
+        const char* e = std::getenv("PBR_DEBUG_BOUNDS_SKEW");
+        return PBR_DEBUG_BOUNDS && e != nullptr && std::atoi(e) != 0;
+    }();
+    return skew;
+}
 
 // Streams a context tracks at once. Contexts expect a small, long-lived set of streams (a FrameResource-style
 // ring); a caller that keeps creating new ones pays one device synchronisation per new stream, and past this
@@ -259,7 +294,7 @@ int pbr_context_create(int device, pbr_context** out_ctx) {
         delete ctx;
         return PBR_ERR_NO_DEVICE;
     }
-    hipError_t e = hipSuccess;
+    hipError_t e = arm_bounds(device);
     for (int i = 0; e == hipSuccess && i < pbr_context::kSlots; ++i) {
         e = hipHostMalloc(reinterpret_cast<void**>(&ctx->slots[i].h), sizeof(pbr_light) * PBR_MAX_LIGHTS,
                           hipHostMallocDefault);
@@ -522,6 +557,8 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
     a.frame.coverage = fr->coverage;
     a.frame.coverage_stride = fr->coverage_row_stride;
     a.frame.sky = ctx->sky.d;
+    a.frame.width = gb->width - (debug_bounds_skew() ? 1 : 0);
+    a.frame.height = gb->height;
     a.ambient_mode = ctx->ambient_mode;
     a.f0_plane = f0_plane;
     a.apply_ao = apply_ao;
@@ -696,6 +733,26 @@ const char* pbr_last_pass_kernel(pbr_context* ctx, void* stream) {
         if (ctx->streams[i].stream == s && ctx->streams[i].tiles > 0) si = (int)i;
     if (si < 0) si = ctx->last_stream;
     return si < 0 ? "" : ctx->streams[si].kernel.c_str();
+}
+
+int pbr_debug_bounds(pbr_context* ctx, uint32_t* flags, int reset) {
+    if (!ctx) return PBR_ERR_INVALID_ARGUMENT;
+    if (!PBR_DEBUG_BOUNDS) return PBR_ERR_UNSUPPORTED;
+    DeviceGuard g(ctx->device);
+    uint32_t* b = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_bounds_mu);
+        b = g_bounds_buf[ctx->device];
+    }
+    if (!g.ok || !b) return PBR_ERR_NOT_READY;
+    uint32_t h[2 * pbr::kBoundsClasses];
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h, b, kBoundsBytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) e = hipMemset(b, 0, kBoundsBytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return fail_hip(ctx, e, "pbr_debug_bounds");
+    if (flags) std::memcpy(flags, h, kBoundsBytes);
+    return PBR_OK;
 }
 
 }  // extern "C"

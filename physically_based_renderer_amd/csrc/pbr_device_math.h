@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include "libm_f32.h"
 #include "libm_f32_x2.h"
+#include "pbr_debug_bounds.h"
 
 namespace pbr {
 
@@ -383,8 +384,9 @@ __device__ __forceinline__ f3 sample_linear_wrap(const float4* __restrict__ env,
     int x0 = wrap_index(x0f, w), y0 = wrap_index(y0f, h);
     int x1 = x0 + 1 == w ? 0 : x0 + 1;
     int y1 = y0 + 1 == h ? 0 : y0 + 1;
-    float4 t00 = env[y0 * w + x0], t10 = env[y0 * w + x1];
-    float4 t01 = env[y1 * w + x0], t11 = env[y1 * w + x1];
+    [[maybe_unused]] const int64_t n = (int64_t)w * h;
+    float4 t00 = env[PBR_BOUNDS(y0 * w + x0, n, kBoundsTexel)], t10 = env[PBR_BOUNDS(y0 * w + x1, n, kBoundsTexel)];
+    float4 t01 = env[PBR_BOUNDS(y1 * w + x0, n, kBoundsTexel)], t11 = env[PBR_BOUNDS(y1 * w + x1, n, kBoundsTexel)];
     return mk3(hlerp(hlerp(t00.x, t10.x, fx), hlerp(t01.x, t11.x, fx), fy),
                hlerp(hlerp(t00.y, t10.y, fx), hlerp(t01.y, t11.y, fx), fy),
                hlerp(hlerp(t00.z, t10.z, fx), hlerp(t01.z, t11.z, fx), fy));

@@ -48,6 +48,7 @@ struct FrameArgs {
     const uint8_t* coverage;   // nullptr = every pixel is geometry; else 0 = background (sky pass)
     int64_t coverage_stride;   // bytes
     const float4* sky;         // sky_w * sky_h RGBA fp32 (required when coverage != nullptr)
+    int width, height;         // the frame (= the G-buffer's; PBR_DEBUG_BOUNDS builds check stores against it)
 };
 
 // One statistics record (int32 each): its fields, summed over the pass by pbr_last_pass_stats.
@@ -93,6 +94,7 @@ int64_t shade_tile_count(int width, int height, int pixels_per_thread);
 int shade_stat_slots_per_tile(int pixels_per_thread);
 hipError_t debug_bal_profile(unsigned long long* out8, bool reset);  // PBR_BAL_PROFILE builds only
 hipError_t debug_wave_timeline(unsigned long long* buf, long long cap);  // PBR_WAVE_TIMELINE builds only
+hipError_t debug_bounds_publish(uint32_t* buf);  // PBR_DEBUG_BOUNDS builds only (pbr_debug_bounds.h)
 hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels, hipStream_t stream);
 
 }  // namespace pbr

@@ -179,7 +179,8 @@ __device__ __forceinline__ int stage_chunk(const float4* __restrict__ lights, in
 struct LightRec {
     float4 s, d, p;
 };
-__device__ __forceinline__ LightRec light_rec(const float4* __restrict__ lights, int j) {
+__device__ __forceinline__ LightRec light_rec(const float4* __restrict__ lights, int j, const PassArgs& ps) {
+    j = PBR_BOUNDS(j, ps.n_dir + ps.n_point + ps.n_spot, kBoundsLight);
     return LightRec{lights[3 * j], lights[3 * j + 1], lights[3 * j + 2]};
 }
 // The light's fast-path window flag (pbr_set_pass writes 1.0f or 0.0f into pad1) as a lane mask, on
@@ -223,8 +224,15 @@ __device__ __forceinline__ void survivor_masks(const float4* __restrict__ lights
     }
 }
 
+// The survivor masks of the first 256 point lights as wave_light_terms found them, for the culled walk to reuse
+// (valid: a pass without spot lights, whose walk over the point lights starts with the same range and box).
+struct FirstSurvivors {
+    uint64_t m[4];
+    bool valid = false;
+};
 __device__ __forceinline__ int wave_light_terms(const float4* __restrict__ lights, const PassArgs& ps,
-                                                const TileBounds& wb, bool cull_enabled) {
+                                                const TileBounds& wb, bool cull_enabled,
+                                                FirstSurvivors* first = nullptr) {
     const int b0 = ps.n_dir, b1 = ps.n_dir + ps.n_point + ps.n_spot;
     if (!cull_enabled) return b1;
     int total = ps.n_dir;
@@ -232,6 +240,10 @@ __device__ __forceinline__ int wave_light_terms(const float4* __restrict__ light
         uint64_t m[4];
         survivor_masks(lights, base, b1, wb, true, m);
         total += __popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]);
+        if (first != nullptr && base == b0 && ps.n_spot == 0) {
+            for (int k = 0; k < 4; ++k) first->m[k] = m[k];
+            first->valid = true;
+        }
     }
     return total;
 }
@@ -252,7 +264,8 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
                                               const TileBounds& wb, bool cull_enabled, m2& redo, int& kept_total,
                                               BalancedWaveLds* bal = nullptr, const float* bal_lights = nullptr,
                                               bool geo_a = false, bool geo_b = false, BalMasks bm = BalMasks{},
-                                              unsigned long long* bal_prof = nullptr) {
+                                              unsigned long long* bal_prof = nullptr,
+                                              const FirstSurvivors* first = nullptr) {
     f3x2 direct = splat3(0.0f, 0.0f, 0.0f);
     Faithful2 fi{};
     if (FAITHFUL) fi = make_faithful<!CULL>(q);
@@ -260,7 +273,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     // out there, it was the register peak of that path.
     const int n_dir = BALANCED && !FAITHFUL ? 0 : ps.n_dir;
     for (int j = 0; j < n_dir; ++j) {  // directional: never culled
-        const LightRec r = light_rec(lights, j);
+        const LightRec r = light_rec(lights, j, ps);
         m2 ok = fast_ok & light_flag(r);
         if (FAITHFUL) {
             directional_faithful_x2<LEAN, !CULL>(q, fi, r.s, r.d, ok, direct);
@@ -276,7 +289,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     auto run_kind = [&](auto spot_tag, int b0, int b1) {
         constexpr bool SPOT = decltype(spot_tag)::value;
         auto point = [&](int j) {
-            const LightRec r = light_rec(lights, j);
+            const LightRec r = light_rec(lights, j, ps);
             m2 ok = fast_ok & light_flag(r);
             // An unlit light adds +0 in the reference; here its lanes carry +-0 (zero attenuation)
             // when inside the window, and every lane outside it is redone.
@@ -294,7 +307,11 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
         }
         for (int base = b0; base < b1; base += 256) {
             uint64_t ms[4];
-            survivor_masks(lights, base, b1, wb, cull_enabled, ms);
+            if (!SPOT && first != nullptr && first->valid && base == b0) {  // wave_light_terms tested these
+                for (int k = 0; k < 4; ++k) ms[k] = first->m[k];
+            } else {
+                survivor_masks(lights, base, b1, wb, cull_enabled, ms);
+            }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 uint64_t m = ms[k];
@@ -387,13 +404,13 @@ __device__ __forceinline__ void lighting_exact_wave(const PixelInvariants& qa, c
     db = mk3(0.0f, 0.0f, 0.0f);
     bool unused = true;
     for (int j = 0; j < ps.n_dir; ++j) {
-        const LightRec r = light_rec(lights, j);
+        const LightRec r = light_rec(lights, j, ps);
         if (need_a) da = add3(da, directional_light<false>(qa, r.s, r.d, unused));
         if (need_b) db = add3(db, directional_light<false>(qb, r.s, r.d, unused));
     }
     const int pt_begin = ps.n_dir, sp_begin = ps.n_dir + ps.n_point, end = sp_begin + ps.n_spot;
     for (int j = pt_begin; j < end; ++j) {
-        const LightRec r = light_rec(lights, j);
+        const LightRec r = light_rec(lights, j, ps);
         const bool spot = j >= sp_begin;
         f3 c;
         if (need_a) {
@@ -420,6 +437,7 @@ __device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArg
                                             bool vector_load) {
     v2 v[15];
     if (vector_load) {  // both pixels exist and the pair is 8-byte aligned in every plane
+        ia = PBR_BOUNDS_PIXEL(ia, gb.width, gb.height, gb.row_stride, 2, kBoundsGBuffer);
 #pragma unroll
         for (int i = 0; i < 15; ++i) {
             if (i == 11 || (i >= 12 && !F0_PLANE)) continue;  // AO: read at the finish (load_ao_pair)
@@ -427,6 +445,8 @@ __device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArg
             v[i] = v2{t.x, t.y};
         }
     } else {
+        ia = PBR_BOUNDS_PIXEL(ia, gb.width, gb.height, gb.row_stride, 1, kBoundsGBuffer);
+        ib = PBR_BOUNDS_PIXEL(ib, gb.width, gb.height, gb.row_stride, 1, kBoundsGBuffer);
 #pragma unroll
         for (int i = 0; i < 15; ++i) {
             if (i == 11 || (i >= 12 && !F0_PLANE)) continue;  // AO: read at the finish (load_ao_pair)
@@ -648,6 +668,7 @@ __device__ __forceinline__ uint32_t unorm8(float c) {
 }
 
 __device__ __forceinline__ void store_pixel(const FrameArgs& fr, int64_t off, float4 c) {
+    off = PBR_BOUNDS_PIXEL(off, fr.width, fr.height, fr.out_stride, 1, kBoundsOutput);
     if (fr.format == kOutRgba8) {
         static_cast<uint32_t*>(fr.out)[off] = unorm8(c.x) | (unorm8(c.y) << 8) | (unorm8(c.z) << 16) | (unorm8(c.w) << 24);
     } else {
@@ -661,7 +682,7 @@ __device__ __forceinline__ void store_pixel(const FrameArgs& fr, int64_t off, fl
 // output alpha (Default.hlsl:160). Geometry pixels only (the sky PS has no clip). Returns whether to store.
 __device__ __forceinline__ bool alpha_keep(const GBufferArgs& gb, int64_t gidx, float4& c) {
     if (!gb.alpha_test) return true;  // uniform
-    const float op = gb.plane[15][gidx];
+    const float op = gb.plane[15][PBR_BOUNDS_PIXEL(gidx, gb.width, gb.height, gb.row_stride, 1, kBoundsGBuffer)];
     if (op - 0.1f < 0.0f) return false;
     c.w = op;
     return true;
@@ -680,7 +701,9 @@ __device__ __forceinline__ void alpha_keep_pair(const GBufferArgs& gb, int64_t g
 
 // Coverage of a pixel: geometry unless the frame has a coverage plane holding 0 there.
 __device__ __forceinline__ bool is_geometry(const FrameArgs& fr, int x, int y) {
-    return fr.coverage == nullptr || fr.coverage[(int64_t)y * fr.coverage_stride + x] != 0;
+    return fr.coverage == nullptr ||
+           fr.coverage[PBR_BOUNDS_PIXEL((int64_t)y * fr.coverage_stride + x, fr.width, fr.height, fr.coverage_stride, 1,
+                                        kBoundsCoverage)] != 0;
 }
 
 // The lane's index in its wave, from the hardware (v_mbcnt) in volatile asm: the compiler can neither CSE it
@@ -742,6 +765,7 @@ __device__ __forceinline__ float4 shade_pixel_exact(const GBufferArgs& gb, const
                                                     const float4* __restrict__ lights, const float4* __restrict__ env,
                                                     int64_t idx, bool need, bool faithful_finish) {
     if (!LANES) idx = need ? idx : 0;
+    idx = PBR_BOUNDS_PIXEL(idx, gb.width, gb.height, gb.row_stride, 1, kBoundsGBuffer);
     const f3 pos = mk3(gb.plane[0][idx], gb.plane[1][idx], gb.plane[2][idx]);
     const f3 n = mk3(gb.plane[3][idx], gb.plane[4][idx], gb.plane[5][idx]);
     const f3 albedo = mk3(gb.plane[6][idx], gb.plane[7][idx], gb.plane[8][idx]);
@@ -971,7 +995,11 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                     const int rl = lane_id_fresh();
                     const int rx = blockIdx.x * kTileW + 2 * (rl & 31);
                     const int ry = blockIdx.y * kTileH + 2 * wave_id + (rl >> 5);
+#if PBR_BAL_EXPERIMENT & 32  // development timing: the reload reads the frame's first pixel pair (cache-resident)
+                    const int64_t rrow = 0 * ((int64_t)ry * gb.row_stride + rx);
+#else
                     const int64_t rrow = (int64_t)ry * gb.row_stride + rx;
+#endif
                     p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? rrow : 0, vb ? rrow + 1 : 0,
                                                       vb && gb.pairs_aligned);
                 };
@@ -1045,12 +1073,14 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     if (APPLY_AO) {
         const int64_t arow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
         if (vb && gb.pairs_aligned) {
-            const float2 t = *reinterpret_cast<const float2*>(gb.plane[11] + arow);
+            const float2 t = *reinterpret_cast<const float2*>(
+                gb.plane[11] + PBR_BOUNDS_PIXEL(arow, gb.width, gb.height, gb.row_stride, 2, kBoundsGBuffer));
             ao_a = t.x;
             ao_b = t.y;
         } else {
-            if (va) ao_a = gb.plane[11][arow];
-            if (vb) ao_b = gb.plane[11][arow + 1];
+            if (va) ao_a = gb.plane[11][PBR_BOUNDS_PIXEL(arow, gb.width, gb.height, gb.row_stride, 1, kBoundsGBuffer)];
+            if (vb)
+                ao_b = gb.plane[11][PBR_BOUNDS_PIXEL(arow + 1, gb.width, gb.height, gb.row_stride, 1, kBoundsGBuffer)];
         }
     }
     float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca;
@@ -1133,6 +1163,7 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         const v2 nn = dot3(p.n, p.n);
         const bool lean_lane = ok_a && ok_b && nn.x <= 1.0f + 0x1p-20f && nn.y <= 1.0f + 0x1p-20f &&
                                on(q2.f0_nonzero.x) && on(q2.f0_nonzero.y);
+        FirstSurvivors first;  // the culled walk reuses the faithful term count's first survivor masks
         if (FAITHFUL) {
             const bool faithful_lane =
                 ok_a && ok_b && p.albedo.x.x >= 0.0f && p.albedo.y.x >= 0.0f && p.albedo.z.x >= 0.0f &&
@@ -1142,7 +1173,7 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
                 p.f0.z.y >= 0.0f;
             faithful_wave = lanes(!faithful_lane) == 0;
             if (CULL && faithful_wave && ps.faithful == 2)
-                faithful_wave = wave_light_terms(lights, ps, wb, cull_enabled) <= kFaithfulMaxTerms;
+                faithful_wave = wave_light_terms(lights, ps, wb, cull_enabled, &first) <= kFaithfulMaxTerms;
         }
         const bool lean_wave = lanes(!lean_lane) == 0;
         TL_RT(3);
@@ -1151,9 +1182,11 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         if (faithful_wave) {
             if (!CULL) faithful_scale(q2);
             if (lean_wave)
-                d2 = lighting_fast<CULL, true, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+                d2 = lighting_fast<CULL, true, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total,
+                                                     nullptr, nullptr, false, false, BalMasks{}, nullptr, &first);
             else
-                d2 = lighting_fast<CULL, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+                d2 = lighting_fast<CULL, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total,
+                                                      nullptr, nullptr, false, false, BalMasks{}, nullptr, &first);
             if (!CULL) faithful_unscale(q2);
         } else if (lean_wave) {
             d2 = lighting_fast<CULL, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
@@ -1173,12 +1206,17 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
             if (APPLY_AO) {
                 const int64_t arow = (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
                 if (vb && gb.pairs_aligned) {
-                    const float2 t = *reinterpret_cast<const float2*>(gb.plane[11] + arow);
+                    const float2 t = *reinterpret_cast<const float2*>(
+                        gb.plane[11] + PBR_BOUNDS_PIXEL(arow, gb.width, gb.height, gb.row_stride, 2, kBoundsGBuffer));
                     ao_a = t.x;
                     ao_b = t.y;
                 } else {
-                    if (va) ao_a = gb.plane[11][arow];
-                    if (vb) ao_b = gb.plane[11][arow + 1];
+                    if (va)
+                        ao_a = gb.plane[11][PBR_BOUNDS_PIXEL(arow, gb.width, gb.height, gb.row_stride, 1,
+                                                             kBoundsGBuffer)];
+                    if (vb)
+                        ao_b = gb.plane[11][PBR_BOUNDS_PIXEL(arow + 1, gb.width, gb.height, gb.row_stride, 1,
+                                                             kBoundsGBuffer)];
                 }
             }
             float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca;
@@ -1295,7 +1333,8 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
     const int x = blockIdx.x * kTileW1 + (tid & (kTileW1 - 1));
     const int y = blockIdx.y * kTileH + (tid / kTileW1);
     const bool valid = (x < gb.width) && (y < gb.height);
-    const int64_t idx = valid ? (int64_t)y * gb.row_stride + x : 0;  // frames are never empty here
+    const int64_t idx = PBR_BOUNDS_PIXEL(valid ? (int64_t)y * gb.row_stride + x : 0, gb.width, gb.height, gb.row_stride,
+                                         1, kBoundsGBuffer);  // frames are never empty here
     const bool geom = valid && is_geometry(fr, x, y);
     const bool any_geometry = fr.coverage == nullptr || __syncthreads_or(geom);
 
@@ -1456,6 +1495,26 @@ hipError_t debug_wave_timeline(unsigned long long* buf, long long cap) {
 #else
     (void)buf;
     (void)cap;
+    return hipErrorNotSupported;
+#endif
+}
+
+// PBR_DEBUG_BOUNDS builds: point this translation unit's kernels at the device's bounds-flag buffer
+// (2 * kBoundsClasses words, pbr_debug_bounds.h; one process-wide buffer per device, current device).
+#if PBR_BAL_TU
+hipError_t debug_bounds_publish_bal(uint32_t* buf) {
+#else
+hipError_t debug_bounds_publish_bal(uint32_t* buf);
+hipError_t debug_bounds_publish(uint32_t* buf) {
+#endif
+#if PBR_DEBUG_BOUNDS
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_bounds_flags), &buf, sizeof(buf));
+#if !PBR_BAL_TU && PBR_SPLIT_BAL
+    if (e == hipSuccess) e = debug_bounds_publish_bal(buf);
+#endif
+    return e;
+#else
+    (void)buf;
     return hipErrorNotSupported;
 #endif
 }

@@ -292,6 +292,15 @@ class ShadingContext:
         fn = getattr(self.lib, "pbr_last_pass_kernel", None)  # absent only from older A/B builds (PBR_LIB_PATH)
         return "" if fn is None else (fn(self._h, ctypes.c_void_p(_stream_handle(stream))) or b"").decode()
 
+    def debug_bounds(self, reset: bool = True) -> dict:
+        """pbr_debug_bounds of a bounds-checked build (PBR_DEBUG_BOUNDS, loaded through PBR_LIB_PATH): synchronises
+        the device and returns {class name: last offending index} for every violated index class (empty: none),
+        then clears the flags when ``reset``. Raises PbrError(PBR_ERR_UNSUPPORTED) on a product build."""
+        flags = (ctypes.c_uint32 * 16)()
+        N.check(self.lib.pbr_debug_bounds(self._h, flags, int(reset)), "pbr_debug_bounds", self._h)
+        names = ("gbuffer", "output", "coverage", "texel", "light", "lds")
+        return {n: int(flags[8 + c]) for c, n in enumerate(names) if flags[c]}
+
     def cull_stats(self, stream=None):
         """(sum of surviving point/spot lights over tiles, tiles) of the last pass ((0, 0) unless it culled)."""
         s, t = ctypes.c_int64(), ctypes.c_int64()

@@ -19,7 +19,7 @@ def test_library_loads_and_exports_every_header_symbol():
         assert hasattr(lib, name), f"{name} declared in pbr_shade.h but not exported"
         assert name in N.SIGNATURES, f"{name} has no ctypes signature"
     assert set(N.SIGNATURES) == set(declared)
-    assert lib.pbr_abi_version() == 7
+    assert lib.pbr_abi_version() == 8
 
 
 def test_exports_are_c_symbols():
