@@ -55,7 +55,8 @@ constexpr int kBalRec = 7;         // float4 per exchanged pixel record
 // Per-wave LDS: the exchange region (one record per lane, then the 128 results) and the count histogram.
 #ifndef PBR_BAL_EXPERIMENT
 #define PBR_BAL_EXPERIMENT 0  // development timing switches, bit flags (0 = product): 1 no pass 2, 2 no atan2f/asinf,
-                              // 4 no IBL block, 8 no finish, 16 no back-face tests
+                              // 4 no IBL block, 8 no finish, 16 no back-face tests, 32 exact reload from a
+                              // cache-resident pair, 64 / 128 no light loop / window checks in the lean kernel
 #endif
 #ifndef PBR_BAL_PROFILE
 #define PBR_BAL_PROFILE 0  // development build: per-phase shader-clock sums (pbr_debug_bal_profile)

@@ -96,23 +96,34 @@ __device__ __forceinline__ bool zero_or_in(float x, float lo, float hi) { return
 #define PBR_POW5_LDS 1
 #endif
 #if PBR_POW5_LDS
-__shared__ pbr_powf_log2_entry g_lds_powf_log2[16];
-__shared__ uint64_t g_lds_exp2f[32];
-__shared__ pbr_atan_seg g_lds_atan_seg[5];  // libm_f32_x2.h: atanf's reduction rows
-static __constant__ pbr_atan_seg pbr_atan_seg_tab[5] = PBR_ATAN_SEG_TABLE_INIT;
-// Every work-item of the block calls this, and a barrier follows before the first pow5.
+// The three tables back to back, 37 chunks of 16 bytes: powf's log2 rows (16 x 16 B), its exp2 words (32 x 8 B),
+// atanf's reduction rows (5 x 16 B). load_libm_tables copies them with one 16-byte load per work-item and a single
+// wait (three separately predicated copies each waited for their own load: three round trips before a wave's
+// G-buffer loads could issue).
+struct alignas(16) LibmTables {
+    pbr_powf_log2_entry log2[16];
+    uint64_t exp2[32];
+    pbr_atan_seg atan[5];  // libm_f32_x2.h
+};
+static_assert(sizeof(LibmTables) == 37 * 16, "one 16-byte chunk per work-item");
+__shared__ LibmTables g_lds_libm;
+static __constant__ LibmTables pbr_libm_tables = {PBR_POWF_LOG2_TABLE_INIT, PBR_EXP2F_TABLE_INIT,
+                                                  PBR_ATAN_SEG_TABLE_INIT};
+// Every work-item of the block calls this, and a barrier follows before the first table read. ATAN: the kernel
+// evaluates the packed WorldToSkyUV (diffuse-IBL ambient); otherwise the atan rows are not copied.
+template <bool ATAN = true>
 __device__ __forceinline__ void load_libm_tables() {
+    constexpr int kChunks = ATAN ? 37 : 32;
     const int t = threadIdx.x;
-    if (t < 16) g_lds_powf_log2[t] = pbr_powf_log2_tab[t];
-    if (t >= 16 && t < 21) g_lds_atan_seg[t - 16] = pbr_atan_seg_tab[t - 16];
-    if (t >= 32 && t < 64) g_lds_exp2f[t - 32] = pbr_exp2f_tab[t - 32];
+    if (t < kChunks) reinterpret_cast<uint4*>(&g_lds_libm)[t] = reinterpret_cast<const uint4*>(&pbr_libm_tables)[t];
 }
-#define PBR_POW5_TABLES g_lds_powf_log2, g_lds_exp2f
-#define PBR_LIBM_LOG2_TAB g_lds_powf_log2
-#define PBR_LIBM_EXP2_TAB g_lds_exp2f
-#define PBR_LIBM_ATAN_TAB g_lds_atan_seg
+#define PBR_POW5_TABLES g_lds_libm.log2, g_lds_libm.exp2
+#define PBR_LIBM_LOG2_TAB g_lds_libm.log2
+#define PBR_LIBM_EXP2_TAB g_lds_libm.exp2
+#define PBR_LIBM_ATAN_TAB g_lds_libm.atan
 #else
 static __constant__ pbr_atan_seg pbr_atan_seg_tab[5] = PBR_ATAN_SEG_TABLE_INIT;
+template <bool ATAN = true>
 __device__ __forceinline__ void load_libm_tables() {}
 #define PBR_POW5_TABLES pbr_powf_log2_tab, pbr_exp2f_tab
 #define PBR_LIBM_LOG2_TAB pbr_powf_log2_tab
@@ -154,12 +165,18 @@ __device__ __forceinline__ float pow_inv_gamma(float c) {
     return pbr_powf(c, kInvGamma);
 }
 // PBR_FLAG_FAITHFUL's gamma encode: exp2(kInvGamma * log2(c)) on the hardware v_log_f32 / v_exp_f32
-// for c in [kFaithfulGammaLo, 1) -- every tonemapped value c/(c+1) of a lit channel but the darkest --
-// and glibc's powf elsewhere. Error vs glibc powf measured exhaustively on the GPU
-// (tests/hip/gamma_probe.hip): DESIGN.md §2 adds it to the faithful bound.
-constexpr float kFaithfulGammaLo = 0x1p-10f;
+// for c in [kFaithfulGammaLo, 1) and for c = +-0 (log2 gives -inf, exp2 +0: powf's own +0), glibc's powf
+// elsewhere. Error vs glibc powf measured exhaustively on the GPU per binade (tests/hip/gamma_probe.hip,
+// profiles/r04/gamma_window_scan.log): <= 5.4e-7 from 2^-10 up, <= 1.04e-6 down to 2^-32, 1.6-2.0e-6 below
+// (the rounding of kInvGamma * log2(c) grows with |log2 c|), hence the window's 2^-32; DESIGN.md §2 adds
+// 1.04e-6 to the faithful bound. (Round 3's window began at 2^-10, which sent nearly every wave of configs 2
+// and 3 through glibc's algorithm for some dark channel.)
+#ifndef PBR_FAITHFUL_GAMMA_LO
+#define PBR_FAITHFUL_GAMMA_LO 0x1p-32f
+#endif
+constexpr float kFaithfulGammaLo = PBR_FAITHFUL_GAMMA_LO;
 __device__ __forceinline__ float pow_inv_gamma_faithful(float c) {
-    if (__builtin_expect(c >= kFaithfulGammaLo && c < 1.0f, 1))
+    if (__builtin_expect((c >= kFaithfulGammaLo && c < 1.0f) || c == 0.0f, 1))
         return __builtin_amdgcn_exp2f(kInvGamma * __builtin_amdgcn_logf(c));
     return pow_inv_gamma(c);
 }

@@ -605,6 +605,9 @@ __device__ __forceinline__ float4 finish_lit(f3 ambient, float ao, f3 direct, co
                                              bool faithful) {
     if (APPLY_AO) ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
     f3 lit = add3(ambient, direct);
+#if PBR_BAL_EXPERIMENT & 8  // development timing: no Reinhard / gamma in faithful waves
+    if (faithful) return make_float4(lit.x, lit.y, lit.z, ps.opacity);
+#endif
     if (faithful) {  // wave-uniform
         lit = mk3(reinhard_faithful(lit.x), reinhard_faithful(lit.y), reinhard_faithful(lit.z));
         return make_float4(pow_inv_gamma_faithful(lit.x), pow_inv_gamma_faithful(lit.y),
@@ -849,7 +852,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     unsigned long long* bal_prof = s.prof[__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6];
     if ((threadIdx.x & 63) < 16) bal_prof[threadIdx.x & 63] = 0;
 #endif
-    load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
+    load_libm_tables<AMBIENT == kAmbientIblDiffuse>();  // powf (+ atanf with IBL) tables -> LDS (pbr_device_math.h)
     if constexpr (BAL != 0) stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light);
     __syncthreads();
 
@@ -876,7 +879,14 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const m2 fast2 = mask2(ok_a, ok_b);
     TL_LOADED();
 
-    PixelInvariants2 q2 = pair_invariants(p, ps, fast2);
+    // The pair's invariants. Balanced variants form them on each path that needs them (their balanced paths build
+    // their own after pass 1, so computing them here left one dead pair_invariants on the common path); the
+    // uniform and culled variants form them here (formed per path, the max-ILP build spilled 20-36 B/lane).
+    PixelInvariants2 q2;
+    if constexpr (BAL == 0) q2 = pair_invariants(p, ps, fast2);
+    auto form_q2 = [&]() {
+        if constexpr (BAL != 0) q2 = pair_invariants(p, ps, fast2);
+    };
 
     // The wave's world-space box (its 64x2 pixels; background pixels excluded): wave64 butterflies,
     // then scalar registers. Non-finite positions disable culling for the wave (the reference's
@@ -910,7 +920,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         // Wave-uniform choice of the light loop.
         const v2 nn = dot3(p.n, p.n);
         const bool lean_lane = ok_a && ok_b && nn.x <= 1.0f + 0x1p-20f && nn.y <= 1.0f + 0x1p-20f &&
-                               on(q2.f0_nonzero.x) && on(q2.f0_nonzero.y);
+                               f0_nonzero(lane(p.f0, 0)) && f0_nonzero(lane(p.f0, 1));  // make_invariants' f0_nonzero
         // PBR_FLAG_FAITHFUL (host-validated: strengths, ambient and env texels >= 0): in a wave inside the
         // fast window whose albedo is >= 0 and F0 in [0, 1] every light's contribution is >= 0, which bounds
         // the error of the faithful divisions in the sum (brdf_faithful_x2). ps.faithful == 2: a culled pass
@@ -928,7 +938,6 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         const bool lean_wave = lanes(!lean_lane) == 0;
         // Untiled faithful waves read rescaled invariants (exact both ways, faithful_scale).
         if (faithful_wave && lean_wave) {
-            if (!CULL) faithful_scale(q2);
             if constexpr (BAL == 1 && !CULL) {
 #if PBR_BAL_PROFILE
                 BAL_PROF_ADD(7, (long long)__builtin_amdgcn_s_memtime() - t_entry);
@@ -960,6 +969,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 BAL_PROF_ADD(8, (long long)__builtin_amdgcn_s_memtime() - t_l1);
 #endif
             } else {
+                form_q2();
+                if (!CULL) faithful_scale(q2);
 #if PBR_BAL_PROFILE
                 const long long t_u0 = (long long)__builtin_amdgcn_s_memtime();
                 BAL_PROF_ADD(11, t_u0 - t_entry);
@@ -974,6 +985,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 #endif
             }
         } else if (faithful_wave) {
+            form_q2();
             if (!CULL) faithful_scale(q2);
             d2 = lighting_fast<CULL, false, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
             if (!CULL) faithful_unscale(q2);
@@ -1013,10 +1025,15 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 q2 = pair_invariants(p, ps, fast2);
                 pos2 = p.pos;
             } else {
+                form_q2();
                 d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
             }
-        } else
+        } else {
+            form_q2();
             d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
+        }
+    } else {
+        form_q2();  // background only: the sky pass reads N
     }
     TL_RT(4);
     const PixelInvariants ua = unpack_invariants(q2, 0), ub = unpack_invariants(q2, 1);
@@ -1138,10 +1155,14 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
                                                  vb && gb.pairs_aligned);
         // shade_pair_wave's per-wave choice of the light loop (BAL 0, every pixel geometry), unchanged.
+#if PBR_BAL_EXPERIMENT & 128  // development timing: no window checks in the lean kernel
+        const bool ok_a = ps.eye_ok, ok_b = ps.eye_ok;
+#else
         const bool ok_a = ps.eye_ok && fast_window_ok(lane(p.pos, 0), lane(p.n, 0), lane(p.albedo, 0),
                                                       lane(p.f0, 0), p.metallic.x, p.roughness.x);
         const bool ok_b = ps.eye_ok && fast_window_ok(lane(p.pos, 1), lane(p.n, 1), lane(p.albedo, 1),
                                                       lane(p.f0, 1), p.metallic.y, p.roughness.y);
+#endif
         const m2 fast2 = mask2(ok_a, ok_b);
         TL_LOADED();
         PixelInvariants2 q2 = pair_invariants(p, ps, fast2);
@@ -1179,6 +1200,11 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         TL_RT(3);
         m2 redo = m2{0, 0};
         f3x2 d2;
+#if PBR_BAL_EXPERIMENT & 64  // development timing: no light loop in the lean kernel
+        if (true) {
+            d2 = f3x2{q2.n.x, q2.n.y, q2.n.z};
+        } else
+#endif
         if (faithful_wave) {
             if (!CULL) faithful_scale(q2);
             if (lean_wave)
@@ -1257,7 +1283,8 @@ __global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBuf
                                                             const float4* __restrict__ lights,
                                                             const float4* __restrict__ env, FrameArgs fr,
                                                             int32_t* __restrict__ tile_kept) {
-    load_libm_tables();  // powf tables -> LDS: the exact finish's gamma, spot cones, the faithful gamma's edges
+    // powf tables -> LDS: the exact finish's gamma, spot cones, the faithful gamma's edges (+ atanf rows with IBL)
+    load_libm_tables<AMBIENT == kAmbientIblDiffuse>();
     __syncthreads();
     lean_wave<AMBIENT, F0_PLANE, APPLY_AO, CULL, FAITHFUL>(gb, ps, lights, env, fr, tile_kept, blockIdx.x,
                                                            blockIdx.y >> 2, blockIdx.y & 3,
@@ -1327,7 +1354,7 @@ __global__ __launch_bounds__(kBlock) void shade_tile1_kernel(GBufferArgs gb, Pas
                                                              int32_t* __restrict__ tile_kept,
                                                              bool exact_only) {
     __shared__ Lds s;
-    load_libm_tables();  // powf tables -> LDS (pbr_device_math.h)
+    load_libm_tables<AMBIENT == kAmbientIblDiffuse>();  // powf (+ atanf with IBL) tables -> LDS (pbr_device_math.h)
     __syncthreads();
     const int tid = threadIdx.x;
     const int x = blockIdx.x * kTileW1 + (tid & (kTileW1 - 1));
