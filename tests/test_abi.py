@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 
@@ -88,6 +89,22 @@ def test_null_arguments_are_rejected_without_a_device():
     assert lib.pbr_last_pass_stats(None, None, None) == -1
     assert lib.pbr_gbuffer_fill(None, 0, 0, None, 0, 1) == -1
     assert lib.pbr_scene_pass(None, 0, None, None) == -1
+    assert lib.pbr_debug_bounds(None, None, 0) == -1
+
+
+def test_bounds_checked_build_loads_and_exports_the_abi():
+    """The PBR_DEBUG_BOUNDS build (_lib/debug_bounds, tests/test_gpu_debug_bounds.py) exports the same C ABI; loaded in
+    a child process through PBR_LIB_PATH, as the GPU test does (one HIP library per process)."""
+    dbg = os.path.join(os.path.dirname(N.LIB_PATH), "debug_bounds", "libpbrshade.so")
+    if not os.path.exists(dbg):
+        pytest.skip("bounds-checked build not built (make -C physically_based_renderer_amd/csrc debug-bounds)")
+    code = ("from physically_based_renderer_amd import _native as N; L = N.lib(); "
+            "missing = [s for s in N.header_symbols() if not hasattr(L, s)]; "
+            "assert not missing, missing; assert L.pbr_abi_version() == 8; "
+            "assert L.pbr_debug_bounds(None, None, 0) == -1; print('ok')")
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "PBR_LIB_PATH": dbg}, capture_output=True,
+                       text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device path")
