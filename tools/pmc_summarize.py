@@ -114,6 +114,8 @@ def main():
     }
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     summary = json.load(open(path)) if os.path.exists(path) else {}
+    for k, v in summary.get(workload, {}).items():  # hand-written annotations (e.g. pair_reread) survive a re-profile
+        entry.setdefault(k, v)
     summary[workload] = entry
     json.dump(summary, open(path, "w"), indent=1)
     print(json.dumps(entry, indent=1))
