@@ -110,17 +110,29 @@ def _dead_peer_worker(rank, world, port, q, how):
 
 @pytest.mark.parametrize("how", ["dies", "hangs"])
 def test_gather_times_out_cleanly_when_a_peer_dies(how):
+    import queue
+
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q, how)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = q.get(timeout=180)
-    for p in procs:
-        p.join(timeout=90)
-        if p.is_alive():
-            p.kill()
+    # A loaded host can stall the two fresh interpreters' rendezvous itself (before any gather: no result at all);
+    # that attempt is abandoned and the scenario run once more on a new port. The assertions are about the gather.
+    for attempt in range(2):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q, how)) for r in range(2)]
+        for p in procs:
+            p.start()
+        try:
+            res = q.get(timeout=120)
+        except queue.Empty:
+            res = None
+        for p in procs:
+            p.join(timeout=90 if res is not None else 1)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+        if res is not None:
+            break
+    assert res is not None, "no rank reported in two attempts (rendezvous never completed)"
     assert res[0] == "GatherError", res
     assert "PBR_DIST_TIMEOUT_S=4" in res[2], res
     # the silent peer sleeps 30 s: rank 0 gave up on its own timeout (4 s) long before it could have exited
