@@ -53,11 +53,6 @@ namespace pbr {
 constexpr int kBalRec = 7;         // float4 per exchanged pixel record
 
 // Per-wave LDS: the exchange region (one record per lane, then the 128 results) and the count histogram.
-#ifndef PBR_BAL_EXPERIMENT
-#define PBR_BAL_EXPERIMENT 0  // development timing switches, bit flags (0 = product): 1 no pass 2, 2 no atan2f/asinf,
-                              // 4 no IBL block, 8 no finish, 16 no back-face tests, 32 exact reload from a
-                              // cache-resident pair, 64 / 128 no light loop / window checks in the lean kernel
-#endif
 #ifndef PBR_BAL_PROFILE
 #define PBR_BAL_PROFILE 0  // development build: per-phase shader-clock sums (pbr_debug_bal_profile)
 #endif
@@ -78,9 +73,15 @@ __device__ unsigned long long* g_bal_prof_buf;  // 16 per wave, wave = block * 4
 
 // The pass's point lights in LDS, structure of arrays (px, py, pz, sx, sy, sz): pass 1 reads four lights'
 // coordinates with one broadcast ds_read_b128 per array, pass 2's two elements read straight into a register
-// pair. Entries [n, kBalLdsStride) are zero: pass 1 may test a padded light (its bit is masked off) and entry
-// kBalMaxLights is the zero strength of an iteration's second element when one light is left.
+// pair. Entries [n, kBalLdsStride) have strength 0: pass 1 may test a padded light (position 0; its bit is masked
+// off) and entry kBalMaxLights is the sentinel of pass 2 (an iteration's second element when one light is left, both
+// elements of a lane with none): strength 0, so its term is (finite) * 0 = +-0, at the position kBalSentinelPos = 2^24
+// on each axis, more than 2.7e7 units from any pixel of the fast window (|P| <= 2^20 per component; the distance, its
+// square and the attenuation stay inside the fast division / sqrt windows), so its window tests (dist >= 0.01,
+// |V + L| >= 2^-30) pass unless V is within ~2^-30 of the direction away from that point: a sentinel item no longer
+// sends a live pixel to the exact re-pass (at position 0 it did for every pixel within 0.01 of the origin).
 constexpr int kBalLdsStride = kBalMaxLights + 4;  // 68 floats: every array 16-byte aligned
+constexpr float kBalSentinelPos = 0x1p24f;
 __device__ __forceinline__ void stage_balanced_lights(const float4* __restrict__ lights, int b0, int b1,
                                                       float* lds_lights) {
     const int t = (int)threadIdx.x;
@@ -89,6 +90,8 @@ __device__ __forceinline__ void stage_balanced_lights(const float4* __restrict__
         if (t < b1 - b0) {
             p = lights[3 * (b0 + t) + 2];
             st = lights[3 * (b0 + t)];
+        } else if (t == kBalMaxLights) {
+            p = make_float4(kBalSentinelPos, kBalSentinelPos, kBalSentinelPos, 0.0f);
         }
         lds_lights[0 * kBalLdsStride + t] = p.x;
         lds_lights[1 * kBalLdsStride + t] = p.y;
@@ -306,7 +309,10 @@ __device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0
 // ComputePointLight (LightingUtil.hlsl:124-142) + BRDFCookTorrance for ONE pixel (q, splat into both elements)
 // and TWO lights (element e: position lp.*[e], strength ls.*[e]), added into `sum`: the operations of
 // point_or_spot_faithful_x2<false, true, true> / brdf_faithful_x2<true, true> element for element (same
-// roundings, same window tests into `ok`).
+// roundings, same window tests into `ok`), but for the Fresnel x^5 (pow5_fast3, three products) and the range cut of
+// LightingUtil.hlsl:131: pass 1 removed every item whose light is beyond the range of its pixel (balanced_pass1), so
+// each item here is within range and the 0/1 factor in_range01 would be exactly 1 (the sentinel's zero strength
+// still zeroes its term).
 __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const f3x2& lp, const f3x2& ls, m2& ok,
                                                       f3x2& sum, uint64_t live) {
     f3x2 l = f3x2{lp.x - q.pos.x, lp.y - q.pos.y, lp.z - q.pos.z};
@@ -315,14 +321,14 @@ __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const 
     const Recip2 rdist = recip_nr(dist);
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     const f3x2 h = normalize_x2(f3x2{q.v.x + l.x, q.v.y + l.y, q.v.z + l.z}, ok);
-    const v2 att = (rdist.r * rdist.r) * in_range01(dist);
+    const v2 att = rdist.r * rdist.r;
     const f3x2 n = splat3(q.n.x, q.n.y, q.n.z);
     const v2 n_dot_h = dot3_sat(n, h);
     const v2 inner = ((n_dot_h * n_dot_h) * q.a2m1 + 1.0f);
     const v2 den = inner * inner;
     const v2 n_dot_l = dot3_sat(n, l);
     const v2 r = rcp_hw((den * vfma(n_dot_l, splat(q.omk), splat(q.k))) * vfma(splat(q.nv), n_dot_l, splat(0.001f)));
-    const v2 p = pow5_faithful(1.0f - dot3_sat(h, splat3(q.v.x, q.v.y, q.v.z)), live);
+    const v2 p = pow5_fast3(1.0f - dot3_sat(h, splat3(q.v.x, q.v.y, q.v.z)), live);
     const f3x2 f = f3x2{q.f0.x + q.omf0.x * p, q.f0.y + q.omf0.y * p, q.f0.z + q.omf0.z * p};
     const v2 kr = (q.a2gv * n_dot_l) * r;
     const v2 w = att * n_dot_l;
@@ -333,7 +339,8 @@ __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const 
 
 // The same two items on the exact lean loop: point_or_spot_x2<false, true> (pbr_device_math_x2.h) for one pixel
 // and two lights, element for element the same operations (the pixel's invariants splat into both elements), so
-// each element's term carries the bits of the uniform loop's term for that (pixel, light).
+// each element's term carries the bits of the uniform loop's term for that (pixel, light), less the range factor,
+// which is exactly 1 for every item pass 1 keeps (faithful_point_items2): the bits are unchanged.
 __device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3x2& lp, const f3x2& ls, m2& ok) {
     PixelInvariants2 q;
     q.n = splat3(p.n.x, p.n.y, p.n.z);
@@ -356,8 +363,7 @@ __device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     const f3x2 h = normalize_x2(add3(q.v, l), ok);
     const v2 dsat = max_dsat(dist);
-    v2 att = recip_nr(dsat * dsat).r;
-    att *= in_range01(dist);
+    const v2 att = recip_nr(dsat * dsat).r;
     return brdf_x2<true>(q, f3x2{ls.x * att, ls.y * att, ls.z * att}, l, h, ok);
 }
 
@@ -366,9 +372,24 @@ struct BalMasks {
     uint32_t a0, a1, c0, c1;  // pixel a: lights [0, 32), [32, 64); pixel b: the same
 };
 
+// The reference's range cut (LightingUtil.hlsl:129-131: d = length(lightVec); if (d > 100) return 0) as pass 1 applies it
+// to a light whose range boundary crosses the wave's box: d = RN(sqrt(x)) with x = dot(l, l) in HLSL order (the kernel's
+// sqrt_nr is the correctly rounded sqrt in the window), and RN(sqrt(x)) <= 100 <=> sqrt(x) <= 100 + 2^-18 (the midpoint
+// to the next float, 2^-17 above 100, rounds to the even 100) <=> x <= (100 + 2^-18)^2 = 10000 + 7.6e-4, below the next
+// float after 10000 (2^-10 above it): d > 100 <=> x > 10000, decided bit for bit as the reference decides it.
+__device__ __forceinline__ m2 beyond_range(const f3x2& pos, float lx, float ly, float lz) {
+    const f3x2 l = f3x2{splat(lx) - pos.x, splat(ly) - pos.y, splat(lz) - pos.z};
+    const v2 x = dot3(l, l);
+    return mask2(x.x > 10000.0f, x.y > 10000.0f);
+}
+
 // Pass 1 for point lights [0, nl) of the pass (staged in `lds_lights`), from the pair's raw G-buffer position
 // and normal (the test is invariant under scaling N): run before the loop invariants exist, so that the two
 // never hold registers at the same time. Wave-uniform control flow.
+// The range cut (LightingUtil.hlsl:131) is applied here too, so pass 2 evaluates no item beyond the range and carries
+// no range test: a light farther than 100 from every pixel of the wave's box is dropped for the wave (its terms are
+// the +0 the reference adds); a light whose range boundary crosses the box is tested per pixel (beyond_range, the
+// reference's own decision), a light within 99.9 of every corner is kept as the back-face test says.
 __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& n, bool live_a, bool live_b, int nl,
                                                    BalancedWaveLds& w, const float* lds_lights,
                                                    unsigned long long* bal_prof = nullptr) {
@@ -392,14 +413,26 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
     const float pmax = bal_wave_max(fmaxf(live_a ? (fabsf(pa.x) + fabsf(pa.y)) + fabsf(pa.z) : 0.0f,
                                           live_b ? (fabsf(pb.x) + fabsf(pb.y)) + fabsf(pb.z) : 0.0f));
     float bj = 0.0f;  // B_j of light j = lane (j < nl; padded lights: zero position, harmless), B = the maximum
+    bool near = true, far = false;  // light j: within range of every pixel of the box / beyond range of every one
     if (lane_id < nl) {
         const float lx = lds_lights[lane_id], ly = lds_lights[kBalLdsStride + lane_id],
                     lz = lds_lights[2 * kBalLdsStride + lane_id];
         const float b0 = ((fabsf(lx - cx) + fabsf(ly - cy)) + fabsf(lz - cz)) + slack;
-        const float far = ((fabsf(lx) + fabsf(ly)) + fabsf(lz)) + pmax;
-        bj = (b0 + 0.125f * far) * (1.0f + 0x1p-20f);
+        const float fr = ((fabsf(lx) + fabsf(ly)) + fabsf(lz)) + pmax;
+        bj = (b0 + 0.125f * fr) * (1.0f + 0x1p-20f);
+        // The box corner farthest from the light (per axis) and the box point nearest to it bound its distance to
+        // every pixel of the wave. In fp32 with a few roundings (~5u) against the kernel's dist, itself within ~5u of
+        // the true distance: a farthest corner <= 99.9 leaves every pixel's d < 100, a nearest point >= 100.1 every
+        // d > 100. Neither holds for a NaN (then, or in between, the pixel test decides).
+        const float fx = fmaxf(fabsf(lx - mnx), fabsf(lx - mxx)), fy = fmaxf(fabsf(ly - mny), fabsf(ly - mxy)),
+                    fz = fmaxf(fabsf(lz - mnz), fabsf(lz - mxz));
+        const float gx = fmaxf(fmaxf(mnx - lx, lx - mxx), 0.0f), gy = fmaxf(fmaxf(mny - ly, ly - mxy), 0.0f),
+                    gz = fmaxf(fmaxf(mnz - lz, lz - mxz), 0.0f);
+        near = (fx * fx + fy * fy) + fz * fz <= 99.9f * 99.9f;
+        far = (gx * gx + gy * gy) + gz * gz >= 100.1f * 100.1f;
     }
     const float bmax = bal_wave_max(bj);
+    const uint64_t far_m = lanes(far), cross_m = lanes(!near && !far);  // bit j: light j (lane j)
     const v2 cn = v2{0x1p-18f * ((fabsf(n.x.x) + fabsf(n.y.x)) + fabsf(n.z.x)),
                      0x1p-18f * ((fabsf(n.x.y) + fabsf(n.y.y)) + fabsf(n.z.y))};
     const v2 nd = -vfma(n.z, pos.z, vfma(n.y, pos.y, n.x * pos.x));  // -N.P
@@ -440,20 +473,32 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
         }
     };
     const int n0 = nl < 32 ? nl : 32;
-#if PBR_BAL_EXPERIMENT & 16  // development timing: no back-face tests (every other light live)
-    a0 = c0 = a1 = c1 = 0xaaaaaaaau;
-    (void)word;
-#else
     if (nl > 32) word(8, a1, c1);
     word(0, a0, c0);
-#endif
-    // Live masks (light j at bit j % 32 of its word); bits above a word's light count are not lights.
+    // Live masks (light j at bit j % 32 of its word); bits above a word's light count are not lights, nor are the
+    // lights beyond range of the whole box (scalar masks: no VALU).
     const int n1 = nl - n0;
-    const uint32_t k0 = n0 == 32 ? ~0u : (1u << n0) - 1u, k1 = n1 == 32 ? ~0u : (1u << n1) - 1u;
+    const uint32_t k0 = (n0 == 32 ? ~0u : (1u << n0) - 1u) & ~(uint32_t)far_m,
+                   k1 = (n1 == 32 ? ~0u : (1u << n1) - 1u) & ~(uint32_t)(far_m >> 32);
     a0 = live_a ? ~a0 & k0 : 0u;
     c0 = live_b ? ~c0 & k0 : 0u;
     a1 = live_a ? ~a1 & k1 : 0u;
     c1 = live_b ? ~c1 & k1 : 0u;
+    // Lights whose range boundary crosses the box: the reference's decision per pixel (rare: none in the BASELINE
+    // scenes, whose lights are within range of every pixel).
+    for (uint64_t cm = cross_m; cm != 0; cm &= cm - 1) {  // uniform
+        const int j = __builtin_ctzll(cm);
+        const m2 out = beyond_range(pos, lds_lights[j], lds_lights[kBalLdsStride + j], lds_lights[2 * kBalLdsStride + j]);
+        const uint32_t bit = 1u << (j & 31);
+        const uint32_t oa = on(out.x) ? bit : 0u, ob = on(out.y) ? bit : 0u;
+        if (j < 32) {
+            a0 &= ~oa;
+            c0 &= ~ob;
+        } else {
+            a1 &= ~oa;
+            c1 &= ~ob;
+        }
+    }
 
     BAL_PROF_T(t1);
     BAL_PROF_ADD(0, t1 - t0);
@@ -558,65 +603,63 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
         accx = mk3(0.0f, 0.0f, 0.0f);
     };
     // First pixels without a live light: hand them back and start the second ones at once (which may have none
-    // either: then they are handed back too, and those lanes run sentinels only).
-    {
-        const uint64_t done = lanes(m == 0);
-        if (done != 0) {  // uniform
-            if (on(done)) {
-                put_result();
-                next_pixel();
-            }
-            second = done;
-            const uint64_t empty = done & lanes(m == 0);
-            if (empty != 0 && on(empty)) put_result();
+    // either: then they are handed back too, and those lanes run sentinels only). `zero`: the lanes whose current
+    // mask is empty, formed by ONE compare per iteration (at its end: the next iteration's live lanes are the rest).
+    uint64_t zero = lanes(m == 0);
+    if (zero != 0) {  // uniform
+        if (on(zero)) {
+            put_result();
+            next_pixel();
         }
+        second = zero;
+        const uint64_t first_done = zero;
+        zero = lanes(m == 0);
+        const uint64_t empty = first_done & zero;
+        if (empty != 0 && on(empty)) put_result();
     }
 #if PBR_BAL_PROFILE
     int iters = 0;
 #endif
-#if PBR_BAL_EXPERIMENT & 1  // timing experiment: no pass 2
-    if (on(~second)) {
-        put_result();
-        next_pixel();
-    }
-    second = ~0ull;
-    if (true) put_result();
-    m = 0;
-#endif
-    while (true) {
-        const uint64_t live = lanes(m != 0);
-        if (live == 0) break;
+    {
+        uint64_t live = ~zero;
+        while (live != 0) {
 #if PBR_BAL_PROFILE
-        ++iters;
+            ++iters;
 #endif
-        // Two live lights per lane (ctz saturating to the sentinel index: v_ffbl of 0 is -1), or the sentinel.
-        const int j0 = m != 0 ? __builtin_ctzll(m) : kBalMaxLights;
-        m &= m - 1;  // no-op when m == 0
-        const int j1 = m != 0 ? __builtin_ctzll(m) : kBalMaxLights;
-        m &= m - 1;
-        m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests, as lane masks
-        f3x2 lp, ls;
-        read_pair_lights(lds_lights, j0, j1, lp, ls);
-        if constexpr (EXACT) {
-            const f3x2 c = exact_point_items2(cur, lp, ls, oki);
-            accx = mk3((accx.x + c.x.x) + c.x.y, (accx.y + c.y.x) + c.y.y, (accx.z + c.z.x) + c.z.y);
-        } else {
-            faithful_point_items2(cur, lp, ls, oki, acc, live);
-        }
-        fail |= ~(oki.x & oki.y) & live;
-        // The lanes whose pixel just ran out of live lights.
-        const uint64_t done = lanes(m == 0) & live;
-        if (done != 0) {  // uniform
-            if (on(done)) {
-                put_result();
-                if (!on(second)) next_pixel();
+            // Two live lights per lane (ctz saturating to the sentinel index: v_ffbl of 0 is -1), or the sentinel.
+            const int j0 = m != 0 ? __builtin_ctzll(m) : kBalMaxLights;
+            m &= m - 1;  // no-op when m == 0
+            const int j1 = m != 0 ? __builtin_ctzll(m) : kBalMaxLights;
+            m &= m - 1;
+            m2 oki = m2{~0ull, ~0ull};  // this item pair's window tests, as lane masks
+            f3x2 lp, ls;
+            read_pair_lights(lds_lights, j0, j1, lp, ls);
+            if constexpr (EXACT) {
+                const f3x2 c = exact_point_items2(cur, lp, ls, oki);
+                accx = mk3((accx.x + c.x.x) + c.x.y, (accx.y + c.y.x) + c.y.y, (accx.z + c.z.x) + c.z.y);
+            } else {
+                faithful_point_items2(cur, lp, ls, oki, acc, live);
             }
-            fail &= ~done;
-            const uint64_t first_done = done & ~second;
-            second |= first_done;
-            // A second pixel with no live light: hand it back now (rare).
-            const uint64_t empty = first_done & lanes(m == 0);
-            if (empty != 0 && on(empty)) put_result();
+            fail |= ~(oki.x & oki.y) & live;
+            // The lanes whose pixel just ran out of live lights.
+            zero = lanes(m == 0);
+            const uint64_t done = zero & live;
+            if (done != 0) {  // uniform
+                if (on(done)) {
+                    put_result();
+                    if (!on(second)) next_pixel();
+                }
+                fail &= ~done;
+                const uint64_t first_done = done & ~second;
+                second |= first_done;
+                if (first_done != 0) {  // those lanes hold their second pixel's mask now
+                    zero = lanes(m == 0);
+                    // A second pixel with no live light: hand it back now (rare).
+                    const uint64_t empty = first_done & zero;
+                    if (empty != 0 && on(empty)) put_result();
+                }
+            }
+            live = ~zero;
         }
     }
     BAL_PROF_T(t3);

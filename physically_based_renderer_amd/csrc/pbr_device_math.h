@@ -363,12 +363,8 @@ __device__ __forceinline__ bool point_or_spot_light(const PixelInvariants& q, f3
 
 // WorldToSkyUV (LightingUtil.hlsl:216-225); .xy only.
 __device__ __forceinline__ void world_to_sky_uv(f3 c, float& u, float& v) {
-#if defined(PBR_BAL_EXPERIMENT) && (PBR_BAL_EXPERIMENT & 2)  // development timing: no atan2f / asinf
-    float ux = c.z * 0.5f + c.x, uy = c.y * 0.5f;
-#else
     float ux = pbr_atan2f(c.z, c.x);  // glibc's algorithms, bit for bit (libm_f32.h)
     float uy = pbr_asinf(c.y);
-#endif
     ux = ux * 0.1591f;
     uy = uy * 0.3183f;
     ux = ux + 0.5f;

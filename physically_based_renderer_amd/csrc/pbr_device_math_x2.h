@@ -333,6 +333,29 @@ __device__ __forceinline__ v2 pow5_faithful(v2 x, uint64_t live = ~0ull) {
     return p;
 }
 
+// Fresnel x^5 of the wave-balanced faithful items (pbr_balanced.h, pass 2): three plain products, x^2, x^4, x^5
+// (each rounded once: within 4u + 6u^2 of x^5, u = 2^-24, so within 5.64u p of glibc's powf, which is within 0.82 ulp
+// <= 1.64u p of x^5), 3 packed ops per pair instead of pow5_faithful's 8. The diffuse factor 1 - F = (1 - F0)(1 - p)
+// sees that difference amplified by p / (1 - p), so glibc's algorithm takes over above x = 0.97 (p = 0.859, factor
+// 6.1): <= 5.64u * 6.1 = 34.4u = 2.05e-6 on a term's diffuse part (pow5_faithful: 1 ulp, <= 1.2e-6 below 0.99; the
+// bound of DESIGN.md §2 carries the difference). Above 0.97, H.V < 0.03: L within ~3.4 degrees of -V, which a live
+// item (N.L > 0, N.V >= 0) reaches only at grazing views, so the branch stays rare. `live` as in pow5_faithful.
+#ifndef PBR_POW5_FAST3_GLIBC_FROM
+#define PBR_POW5_FAST3_GLIBC_FROM 0.97f
+#endif
+__device__ __forceinline__ v2 pow5_fast3(v2 x, uint64_t live) {
+    const v2 x2 = x * x;
+    const v2 x4 = x2 * x2;
+    v2 p = x4 * x;
+    if (__builtin_expect((lanes(x.x > PBR_POW5_FAST3_GLIBC_FROM) & live) != 0, 0)) {
+        if (x.x > PBR_POW5_FAST3_GLIBC_FROM && on(live)) p.x = pow5_glibc(x.x);
+    }
+    if (__builtin_expect((lanes(x.y > PBR_POW5_FAST3_GLIBC_FROM) & live) != 0, 0)) {
+        if (x.y > PBR_POW5_FAST3_GLIBC_FROM && on(live)) p.y = pow5_glibc(x.y);
+    }
+    return p;
+}
+
 // SCALED (the untiled kernels): the loop runs on invariants rescaled by powers of two (faithful_scale) and
 // the Smith and specular denominators are FMAs. Unscaled (tiled culling, where a wave sums a handful of
 // lights and the per-pixel rescaling does not pay for itself; measured 4% slower on config 4) keeps the

@@ -518,9 +518,6 @@ __device__ __forceinline__ float reinhard_faithful(float c) { return c * __built
 template <int AMBIENT>
 __device__ __forceinline__ f3 ambient_term(const PixelInvariants& p, const PassArgs& ps, const float4* __restrict__ env) {
     const PixelInvariants& q = p;
-#if PBR_BAL_EXPERIMENT & 4  // development timing: no IBL block
-    if (AMBIENT == kAmbientIblDiffuse) return mk3(p.albedo.x * 0.5f, p.albedo.y * 0.5f, p.albedo.z * 0.5f);
-#endif
     if (AMBIENT == kAmbientIblDiffuse) {
         // Default.hlsl:141-146: kS = FresnelSchlick(N, V, F0); kD = (1 - kS)(1 - metallic);
         // irradiance = env.Sample(linear-wrap, WorldToSkyUV(N)); ambient = kD * (irradiance * albedo)
@@ -549,9 +546,6 @@ __device__ __forceinline__ f3 ambient_term(const PixelInvariants& p, const PassA
 __device__ __forceinline__ f3x2 ambient_ibl_pair(const PixelInvariants2& q, const PassArgs& ps,
                                                const float4* __restrict__ env, bool faithful, bool live_a,
                                                bool live_b) {
-#if PBR_BAL_EXPERIMENT & 4  // development timing: no IBL block
-    return f3x2{q.albedo.x * 0.5f, q.albedo.y * 0.5f, q.albedo.z * 0.5f};
-#endif
     const v2 x = 1.0f - dot3_sat(q.n, q.v);  // 1 - saturate(dot(N, V)): the clamp bit maps NaN to 0 as hsat
     const v2 pw = faithful ? pow5_faithful(x, lanes(live_a || live_b)) : v2{pow5_glibc(x.x), pow5_glibc(x.y)};
     const f3x2 kd = f3x2{(1.0f - (q.f0.x + q.one_minus_f0.x * pw)) * q.one_minus_metal,
@@ -559,13 +553,8 @@ __device__ __forceinline__ f3x2 ambient_ibl_pair(const PixelInvariants2& q, cons
                          (1.0f - (q.f0.z + q.one_minus_f0.z * pw)) * q.one_minus_metal};
     // WorldToSkyUV (LightingUtil.hlsl:216-225)
     int sa[2], sb[2];
-#if PBR_BAL_EXPERIMENT & 2  // development timing: no atan2f / asinf
-    v2 ux = q.n.z * 0.5f + q.n.x, uy = q.n.y * 0.5f;
-    sa[0] = sa[1] = sb[0] = sb[1] = 0;
-#else
     v2 ux = pbr_atan2f_x2(q.n.z, q.n.x, sa, PBR_LIBM_ATAN_TAB);
     v2 uy = pbr_asinf_x2(q.n.y, sb);
-#endif
     const bool spec_a = live_a && (sa[0] | sb[0]), spec_b = live_b && (sa[1] | sb[1]);
     if (__builtin_expect(lanes(spec_a || spec_b) != 0, 0)) {
         if (spec_a) {
@@ -605,9 +594,6 @@ __device__ __forceinline__ float4 finish_lit(f3 ambient, float ao, f3 direct, co
                                              bool faithful) {
     if (APPLY_AO) ambient = mk3(ambient.x * ao, ambient.y * ao, ambient.z * ao);
     f3 lit = add3(ambient, direct);
-#if PBR_BAL_EXPERIMENT & 8  // development timing: no Reinhard / gamma in faithful waves
-    if (faithful) return make_float4(lit.x, lit.y, lit.z, ps.opacity);
-#endif
     if (faithful) {  // wave-uniform
         lit = mk3(reinhard_faithful(lit.x), reinhard_faithful(lit.y), reinhard_faithful(lit.z));
         return make_float4(pow_inv_gamma_faithful(lit.x), pow_inv_gamma_faithful(lit.y),
@@ -637,9 +623,6 @@ __device__ __forceinline__ void finish_pair(const PixelInvariants2& q2, const Pi
 template <int AMBIENT, bool APPLY_AO>
 __device__ __forceinline__ float4 finish_pixel(const PixelInvariants& p, float ao, f3 direct, const PassArgs& ps,
                                                const float4* __restrict__ env, bool fast, bool faithful = false) {
-#if PBR_BAL_EXPERIMENT & 8  // development timing: no finish in faithful waves
-    if (faithful) return make_float4(direct.x, direct.y, direct.z, 1.0f);
-#endif
     return finish_lit<APPLY_AO>(ambient_term<AMBIENT>(p, ps, env), ao, direct, ps, fast, faithful);
 }
 
@@ -1007,11 +990,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                     const int rl = lane_id_fresh();
                     const int rx = blockIdx.x * kTileW + 2 * (rl & 31);
                     const int ry = blockIdx.y * kTileH + 2 * wave_id + (rl >> 5);
-#if PBR_BAL_EXPERIMENT & 32  // development timing: the reload reads the frame's first pixel pair (cache-resident)
-                    const int64_t rrow = 0 * ((int64_t)ry * gb.row_stride + rx);
-#else
                     const int64_t rrow = (int64_t)ry * gb.row_stride + rx;
-#endif
                     p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? rrow : 0, vb ? rrow + 1 : 0,
                                                       vb && gb.pairs_aligned);
                 };
@@ -1155,14 +1134,10 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
                                                  vb && gb.pairs_aligned);
         // shade_pair_wave's per-wave choice of the light loop (BAL 0, every pixel geometry), unchanged.
-#if PBR_BAL_EXPERIMENT & 128  // development timing: no window checks in the lean kernel
-        const bool ok_a = ps.eye_ok, ok_b = ps.eye_ok;
-#else
         const bool ok_a = ps.eye_ok && fast_window_ok(lane(p.pos, 0), lane(p.n, 0), lane(p.albedo, 0),
                                                       lane(p.f0, 0), p.metallic.x, p.roughness.x);
         const bool ok_b = ps.eye_ok && fast_window_ok(lane(p.pos, 1), lane(p.n, 1), lane(p.albedo, 1),
                                                       lane(p.f0, 1), p.metallic.y, p.roughness.y);
-#endif
         const m2 fast2 = mask2(ok_a, ok_b);
         TL_LOADED();
         PixelInvariants2 q2 = pair_invariants(p, ps, fast2);
@@ -1200,11 +1175,6 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         TL_RT(3);
         m2 redo = m2{0, 0};
         f3x2 d2;
-#if PBR_BAL_EXPERIMENT & 64  // development timing: no light loop in the lean kernel
-        if (true) {
-            d2 = f3x2{q2.n.x, q2.n.y, q2.n.z};
-        } else
-#endif
         if (faithful_wave) {
             if (!CULL) faithful_scale(q2);
             if (lean_wave)

@@ -54,10 +54,14 @@ def all_bands(height: int, world: int, align: int = 8) -> List[Band]:
 
 
 # Failure detection (the reference polls GetDeviceRemovedReason around every Draw step,
-# PBRApp.cpp:247): every collective of the process group -- the band gather included -- gives up after this many
-# seconds instead of blocking on a dead peer until the backend's default (30 min). RCCL's watchdog then aborts
-# the communicator and the process exits non-zero; gloo raises, and BandGather.wait turns that into GatherError.
+# PBRApp.cpp:247): the band gather gives up after PBR_DIST_TIMEOUT_S seconds instead of blocking on a dead peer until
+# the backend's default (30 min). It runs on its own process group (gather_group) created with that timeout; RCCL's
+# watchdog then aborts the communicator and the process exits non-zero, gloo raises, and BandGather.wait turns that
+# into GatherError. The default group -- the rendezvous, barriers, the bench's max-over-ranks all-reduce -- waits at
+# least RENDEZVOUS_TIMEOUT_S, so that ranks whose interpreters start seconds apart (each imports torch first) still
+# meet even when the gather timeout is short.
 DEFAULT_TIMEOUT_S = 300.0
+RENDEZVOUS_TIMEOUT_S = 120.0
 
 
 class GatherError(RuntimeError):
@@ -65,7 +69,7 @@ class GatherError(RuntimeError):
 
 
 def collective_timeout() -> datetime.timedelta:
-    """The process group's collective timeout: PBR_DIST_TIMEOUT_S seconds (default DEFAULT_TIMEOUT_S)."""
+    """The band gather's timeout: PBR_DIST_TIMEOUT_S seconds (default DEFAULT_TIMEOUT_S)."""
     return datetime.timedelta(seconds=float(os.environ.get("PBR_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S)))
 
 
@@ -73,19 +77,39 @@ def init_from_env(backend: str, always: bool = False, timeout: Optional[datetime
                   ) -> Tuple[int, int, int]:
     """(rank, world, local_rank) from torchrun's environment; initialises the default group once: at
     world > 1, and at world 1 too when ``always`` (so a single-rank run exercises the same RCCL
-    communicator init / teardown and collectives as the multi-GPU one). ``timeout`` (default
-    collective_timeout()) bounds every collective: a dead peer ends the run with an error, not a hang."""
+    communicator init / teardown and collectives as the multi-GPU one). ``timeout`` (default: the larger of
+    collective_timeout() and RENDEZVOUS_TIMEOUT_S) bounds the rendezvous and the default group's collectives.
+    Rendezvous: PBR_DIST_INIT_METHOD when set (e.g. ``file:///tmp/run/rdzv``, a file store that needs no free TCP
+    port), else MASTER_ADDR / MASTER_PORT (env://)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if (world > 1 or always) and not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29517")
-        kwargs = {"timeout": timeout if timeout is not None else collective_timeout()}
+        if timeout is None:
+            timeout = max(collective_timeout(), datetime.timedelta(seconds=RENDEZVOUS_TIMEOUT_S))
+        kwargs = {"timeout": timeout}
+        method = os.environ.get("PBR_DIST_INIT_METHOD")
+        if method:
+            kwargs["init_method"] = method
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", local)  # one GPU per rank (RCCL)
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
     return rank, world, local
+
+
+_gather_group = None
+
+
+def gather_group():
+    """The process group the band gather runs on: every rank, with collective_timeout() (created once per
+    process, collectively: every rank calls it the first time it builds a BandGather). None at world 1."""
+    global _gather_group
+    if _gather_group is None and dist.is_initialized() and dist.get_world_size() > 1:
+        _gather_group = dist.new_group(timeout=collective_timeout())
+    return _gather_group
 
 
 class BandGather:
@@ -98,7 +122,7 @@ class BandGather:
 
     def __init__(self, band: Band, width: int, device, group=None, dtype=torch.float32):
         self.band = band
-        self.group = group
+        self.group = group if group is not None else gather_group()
         self.width = width
         self.frame: Optional[torch.Tensor] = None
         if band.rank == 0:
@@ -106,7 +130,7 @@ class BandGather:
         # gloo cannot move device tensors point to point: stage through host memory (tests only;
         # the benchmark's multi-GPU path is RCCL).
         self.host_staged = (band.world > 1 and torch.device(device).type == "cuda"
-                            and dist.get_backend(group) == "gloo")
+                            and dist.get_backend(self.group) == "gloo")
 
     def start(self, band_out: torch.Tensor):
         """Post the gather of ``band_out`` ((rows_max, W, 4)); returns the list of work handles."""

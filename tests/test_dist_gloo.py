@@ -6,7 +6,7 @@ With no GPU here the per-band shading is the CPU oracle -- this test covers the 
 and the gather; the GPU band kernel itself is covered by test_gpu_parity.py::test_row_band_equals_full_frame.
 """
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -16,10 +16,12 @@ import torch.multiprocessing as mp
 from conftest import ROOT
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _rendezvous():
+    """A file-store rendezvous (PBR_DIST_INIT_METHOD) in a fresh directory: no TCP port is picked here and bound later
+    by the children, so two runs cannot race for one (the old free-port probe closed its socket before the ranks
+    bound it). The caller keeps the TemporaryDirectory alive until the ranks have joined."""
+    d = tempfile.TemporaryDirectory(prefix="pbr_rdzv_")
+    return d, "file://" + os.path.join(d.name, "store")
 
 
 def _oracle_band(cfg, band, pc, env):
@@ -32,12 +34,11 @@ def _oracle_band(cfg, band, pc, env):
     return O.shade(list(planes), ops, pc.light_array(), env, n_threads=2)
 
 
-def _worker(rank, world, port, height, q):
+def _worker(rank, world, init, height, q):
     import sys
 
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+    os.environ.update(PBR_DIST_INIT_METHOD=init, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.distributed as dist
 
     from physically_based_renderer_amd import dist as D
@@ -66,35 +67,50 @@ def test_row_bands_gather_equals_single_frame(world, height):
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, height, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    frame = q.get(timeout=240)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    tmp, init = _rendezvous()
+    with tmp:
+        procs = [ctx.Process(target=_worker, args=(r, world, init, height, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        frame = q.get(timeout=240)
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
     cfg = S.CONFIGS[3].with_size(72, height)
     whole = _oracle_band(cfg, D.band_rows(height, 1, 0), S.scene_pass(cfg), S.env_map())
     assert frame.shape == whole.shape
     assert np.array_equal(frame.view(np.uint32), whole.view(np.uint32))
 
 
-def _dead_peer_worker(rank, world, port, q, how):
+def _dead_peer_worker(rank, world, init, q, how):
     """Rank 1 joins the group and then dies (or hangs) before it sends its band; rank 0's gather must give up with
-    GatherError -- at once for a lost connection, within the process group's timeout (PBR_DIST_TIMEOUT_S, here
-    4 s) for a silent peer -- not block."""
+    GatherError -- at once for a lost connection, within the gather's timeout (PBR_DIST_TIMEOUT_S, here 4 s) for a
+    silent peer -- not block. The rendezvous itself runs under the default group's longer timeout
+    (dist.RENDEZVOUS_TIMEOUT_S), so the two interpreters may start seconds apart; a failure anywhere before the
+    gather is reported on the queue, never swallowed."""
     import sys
     import time
+    import traceback
+
+    def report(*item):
+        # multiprocessing.Queue.put only hands the item to a feeder thread; flush it before os._exit ends the process
+        # (an unflushed put was the old "rendezvous stall": rank 0 had its result but died before writing it)
+        q.put(item)
+        q.close()
+        q.join_thread()
 
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), PBR_DIST_TIMEOUT_S="4")
-    from physically_based_renderer_amd import dist as D
+    os.environ.update(PBR_DIST_INIT_METHOD=init, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      PBR_DIST_TIMEOUT_S="4")
+    try:
+        from physically_based_renderer_amd import dist as D
 
-    D.init_from_env("gloo")
-    band = D.band_rows(16, world, rank)
-    g = D.BandGather(band, 8, "cpu")
+        D.init_from_env("gloo")
+        band = D.band_rows(16, world, rank)
+        g = D.BandGather(band, 8, "cpu")
+    except BaseException:  # noqa: BLE001 -- reported to the test instead of a silent missing result
+        report("setup failed", rank, traceback.format_exc())
+        os._exit(3)
     if rank == 1:
         if how == "hangs":
             time.sleep(30)
@@ -102,37 +118,27 @@ def _dead_peer_worker(rank, world, port, q, how):
     t0 = time.perf_counter()
     try:
         D.BandGather.wait(g.start(torch.zeros((band.rows_max, 8, 4))))
-        q.put(("no error", time.perf_counter() - t0))
+        report("no error", time.perf_counter() - t0)
     except D.GatherError as e:
-        q.put(("GatherError", time.perf_counter() - t0, str(e)))
+        report("GatherError", time.perf_counter() - t0, str(e))
     os._exit(0)
 
 
 @pytest.mark.parametrize("how", ["dies", "hangs"])
 def test_gather_times_out_cleanly_when_a_peer_dies(how):
-    import queue
-
     ctx = mp.get_context("spawn")
-    # A loaded host can stall the two fresh interpreters' rendezvous itself (before any gather: no result at all);
-    # that attempt is abandoned and the scenario run once more on a new port. The assertions are about the gather.
-    for attempt in range(2):
-        q = ctx.Queue()
-        port = _free_port()
-        procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q, how)) for r in range(2)]
+    q = ctx.Queue()
+    tmp, init = _rendezvous()
+    with tmp:
+        procs = [ctx.Process(target=_dead_peer_worker, args=(r, 2, init, q, how)) for r in range(2)]
         for p in procs:
             p.start()
-        try:
-            res = q.get(timeout=120)
-        except queue.Empty:
-            res = None
+        res = q.get(timeout=240)
         for p in procs:
-            p.join(timeout=90 if res is not None else 1)
+            p.join(timeout=90)
             if p.is_alive():
                 p.kill()
                 p.join(timeout=10)
-        if res is not None:
-            break
-    assert res is not None, "no rank reported in two attempts (rendezvous never completed)"
     assert res[0] == "GatherError", res
     assert "PBR_DIST_TIMEOUT_S=4" in res[2], res
     # the silent peer sleeps 30 s: rank 0 gave up on its own timeout (4 s) long before it could have exited

@@ -226,6 +226,52 @@ def test_balanced_after_directional_lights(mode, ctx_pair, gpu):
     check_mode(mode, got, want, ref)
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_balanced_range_cut_in_pass1(mode, ctx_pair, gpu):
+    """The range cut `if (d > 100) return 0` (LightingUtil.hlsl:131) as pass 1 applies it (balanced_pass1): lights
+    beyond 100.1 of a wave's whole box are dropped for the wave, lights within 99.9 of every corner are kept, and a
+    light whose range boundary crosses the box is decided per pixel by the reference's own test, dot(l, l) > 10000
+    (beyond_range). Waves (64 x 2 pixels each) here:
+    * rows 0-1: a small cluster, 22 lights within 40 units, 2 lights ~300 units away (dropped whole);
+    * rows 2-3: pixels facing light 0 at exactly 100 + k 2^-17 (k in [-16, 16)) from it -- the cut at ulp
+      granularity -- and the rest of the row nearby (light 0 crosses this box);
+    * rows 4-7: positions spread over a 300-unit box (most lights cross it).
+    Exact mode: bit-identical to the uniform loop and the oracle; faithful: 1e-5 of the oracle."""
+    rng = np.random.default_rng(23)
+    w, h, nl = 128, 8, 24
+    planes, lights = _scene(rng, w, h, nl)
+    planes[0:3, 0:2] = rng.uniform(-2, 2, (3, 2, w))
+    lights[:nl - 2, 8:11] = rng.uniform(-20, 20, (nl - 2, 3))
+    lights[nl - 2:, 8:11] = (300.0, 0.0, 0.0), (0.0, -290.0, 10.0)
+    lights[0, 8:11] = (100.0, 0.0, 0.0)
+    k = np.arange(-16, 16, dtype=np.float32)
+    for r in (2, 3):
+        planes[0:3, r] = rng.uniform(-1, 1, (3, w))
+        planes[0, r, :32] = -k * np.float32(2.0 ** -17)  # l.x = 100 + k ulp(100), l.y = l.z = 0
+        planes[1:3, r, :32] = 0.0
+        planes[3:6, r, :32] = np.array([1.0, 0.0, 0.0], np.float32)[:, None]
+    planes[0:3, 4:8] = rng.uniform(-150, 150, (3, 4, w))
+    flags = N.PBR_FLAG_FAITHFUL if mode == "faithful" else 0
+    pc = PassConstants(num_point_lights=nl, lights_array=lights, flags=flags)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc)
+    st = bal.pass_stats()
+    want, redo_p = run(plain, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    # the cut is exercised: light 0 alone reaches half of the straddling pixels
+    only0 = PassConstants(num_point_lights=1, lights_array=lights[:1], flags=flags)
+    row = np.ascontiguousarray(planes[:, 2:3, :32])
+    ref0 = O.shade(list(row), oracle_pass_from_constants(only0), only0.light_array(), None)
+    dark0 = O.shade(list(row), oracle_pass_from_constants(PassConstants(flags=flags)), None, None)
+    lit0 = ~np.all(ref0[0] == dark0[0], axis=-1)
+    assert 0 < lit0.sum() < 32
+    print(f"range cut ({mode}): light terms {st['light_terms']} of {st['backface_tests']} tests, redo {redo_b} vs {redo_p}")
+    assert st["light_terms"] < st["backface_tests"] // 2  # the far lights and the 300-unit waves' cut items are gone
+    assert redo_b <= redo_p
+    check_mode(mode, got, want, ref)
+
+
 def test_balanced_light_outside_window_sends_all_to_exact(ctx_pair, gpu):
     """A light whose position is outside the fast-path window (|x| > 2^20): every pixel is redone exactly,
     as in the uniform loop (frames bit-identical to the oracle there)."""

@@ -7,9 +7,9 @@ max-over-ranks timing) under torch.distributed.run.
 """
 import json
 import os
-import socket
 import subprocess
 import sys
+import tempfile
 
 import numpy as np
 import pytest
@@ -23,16 +23,15 @@ pytestmark = pytest.mark.gpu
 WIDTH, HEIGHT = 200, 203  # ragged: bands of 8-row tiles plus a short tail
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+# Rendezvous without a pre-picked TCP port (a port probed free here and bound later by the ranks can be taken in
+# between): the spawned ranks meet in a file store (PBR_DIST_INIT_METHOD), torchrun runs --standalone (it picks its
+# own free port for its rendezvous and hands it to the ranks).
+TORCHRUN = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--standalone", "--local-addr", "127.0.0.1"]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, init, q):
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+    os.environ.update(PBR_DIST_INIT_METHOD=init, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.distributed as dist
 
     from physically_based_renderer_amd import dist as D
@@ -55,6 +54,8 @@ def _worker(rank, world, port, q):
     frame = g.assembled(cfg.height)
     if rank == 0:
         q.put(frame.cpu().numpy().copy())
+        q.close()
+        q.join_thread()  # flushed before the process can end
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,14 +67,15 @@ def test_eight_ranks_on_one_gpu_equal_single_frame(gpu):
     world = 8
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    frame = q.get(timeout=300)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    with tempfile.TemporaryDirectory(prefix="pbr_rdzv_") as tmp:
+        procs = [ctx.Process(target=_worker, args=(r, world, "file://" + os.path.join(tmp, "store"), q))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        frame = q.get(timeout=300)
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
     cfg = S.CONFIGS[3].with_size(WIDTH, HEIGHT)
     with ShadingContext(0) as sc:
         sc.set_pass(S.scene_pass(cfg))
@@ -86,9 +88,7 @@ def test_eight_ranks_on_one_gpu_equal_single_frame(gpu):
 def test_bench_multi_rank_rehearsal(gpu):
     """bench.py at N = 4 (gloo, the one GPU shared): one JSON line from rank 0 with the gathered bands'
     checksums matching and the per-rank band geometry of config 5."""
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+    cmd = TORCHRUN + ["--nproc-per-node", "4", os.path.join(ROOT, "bench.py"),
            "--gpus", "4", "--steps", "3", "--warmup", "1", "--ramp-ms", "0", "--dist-backend", "gloo",
            "--rows-per-rank", "64"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
@@ -115,9 +115,7 @@ def test_bench_multi_rank_rehearsal(gpu):
 
 
 def _bench_torchrun(nproc, extra, timeout=600):
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+    cmd = TORCHRUN + ["--nproc-per-node", str(nproc), os.path.join(ROOT, "bench.py"),
            "--gpus", str(nproc), "--steps", "3", "--warmup", "1", "--ramp-ms", "0"] + extra
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT,
                        env={**os.environ, "OMP_NUM_THREADS": "2"})

@@ -149,14 +149,11 @@ def test_native_timed_run(driver, gpu, mode):
 
 
 def _torchrun_native(driver, nproc, *args, timeout=300):
-    import socket
     import sys
 
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "--no-python", driver, *map(str, args)]
+    # --standalone: torchrun picks its own free rendezvous port (no port probed here and bound later)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--standalone", "--local-addr", "127.0.0.1",
+           "--nproc-per-node", str(nproc), "--no-python", driver, *map(str, args)]
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
 
 
