@@ -48,6 +48,10 @@ FLOP_RANGE_TEST = 9  # per light and tile under tiled culling (box distance + co
 PARITY_REL_TOL = 1e-5
 PARITY_RGBA8_CODE_TOL = 1
 EXIT_PARITY = 3  # bench.py's exit status when the checked frame misses the bar (no metric line is printed)
+EXIT_PROVENANCE = 4  # ... when the loaded library is not the product build of this checkout (without --dev)
+# Environment variables that only route the transport of the multi-rank run; every other PBR_* variable changes which
+# library or kernel runs (PBR_LIB_PATH, PBR_BALANCED_MIN, PBR_LEAN, PBR_PIXELS_PER_THREAD, ...): a development setting.
+ENV_NEUTRAL = ("PBR_DIST_TIMEOUT_S", "PBR_DIST_INIT_METHOD")
 
 
 def log(*a):
@@ -55,14 +59,43 @@ def log(*a):
 
 
 def bytes_per_pixel(pc, out_bytes: int = 16) -> int:
-    """Algorithmic HBM bytes per shaded pixel: the planes the kernel reads + the RGBA write
-    (16 B fp32, 4 B RGBA8)."""
+    """Algorithmic HBM bytes per shaded pixel, SURVEY 8(d)'s model: the 12 G-buffer planes of the north star's
+    G-buffer (position, normal, albedo, metallic, roughness, AO: 48 B), + the F0 plane (12 B) when the pass reads it,
+    + the RGBA write (16 B fp32, 4 B RGBA8): 64 B/px for configs 1-3 and 5, 76 B/px for config 4."""
+    planes = 12
+    if pc.flags & N.PBR_FLAG_F0_PLANE:
+        planes += 3
+    return planes * 4 + out_bytes
+
+
+def bytes_read_per_pixel(pc, out_bytes: int = 16) -> int:
+    """The bytes the kernel itself moves per pixel: the AO plane only with PBR_FLAG_APPLY_AO (the reference never
+    reads its AO slot), so 60 B/px where 8(d) counts 64."""
     planes = 11  # pos xyz, normal xyz, albedo rgb, metallic, roughness
     if pc.flags & N.PBR_FLAG_APPLY_AO:
         planes += 1
     if pc.flags & N.PBR_FLAG_F0_PLANE:
         planes += 3
     return planes * 4 + out_bytes
+
+
+def library_provenance(dev: bool) -> dict:
+    """The build the process LOADED (pbr_build_info, ABI 9) against this checkout: its sources stamp, flavor and units,
+    the checkout's stamp, and the reasons it is not the product build of this checkout (`problems`: units of
+    different sources, another checkout, a debug / variant / EXTRA-flags build, PBR_* development overrides in the
+    environment). Empty problems = the measured binary is the one the committed sources describe."""
+    info = N.build_info()
+    tree = N.kernel_sources_sha()
+    problems = N.build_problems(info, tree)
+    overrides = {k: v for k, v in sorted(os.environ.items()) if k.startswith("PBR_") and k not in ENV_NEUTRAL}
+    if overrides:
+        problems.append("development environment overrides: " + ", ".join(f"{k}={v}" for k, v in overrides.items()))
+    if os.path.abspath(N.LIB_PATH) != os.path.abspath(os.path.join(N.PKG_DIR, "_lib", "libpbrshade.so")):
+        problems.append(f"not the in-tree library: {N.LIB_PATH}")
+    return {"path": os.path.relpath(os.path.abspath(N.LIB_PATH), ROOT), "sources_sha": info.get("sources_sha"),
+            "flavor": info.get("flavor"), "tree_sources_sha": tree, "problems": problems, "dev": dev,
+            "units": [{k: u[k] for k in ("unit", "sources_sha", "flavor", "cflags")} for u in info.get("units", [])],
+            "env_overrides": overrides}
 
 
 FLOP_DIR = FLOP_POINT - 17  # 74 per directional light (no distance / attenuation)
@@ -101,12 +134,12 @@ def executed_flops_per_pixel(pc, st: dict, px: int) -> float:
     return round(f / max(px, 1), 2)
 
 
-def load_pmc(workload: str, path: str = os.path.join(ROOT, "profiles", "pmc_summary.json")):
+def load_pmc(workload: str, head: str, path: str = os.path.join(ROOT, "profiles", "pmc_summary.json")):
     """(HBM bytes per launch, VALU-issue busy fraction, provenance) from the committed rocprofv3 PMC summary of
     this workload (profiles/pmc_summary.json, tools/pmc_summarize.py). The counters are quoted only when the
-    summary's kernel_sources_sha equals the hash of the kernel sources this run is built from; otherwise
-    (a kernel changed since the profile, or an unstamped profile) they are None and the provenance says so."""
-    head = N.kernel_sources_sha()
+    summary's kernel_sources_sha -- the stamp of the library the profiled process loaded -- equals `head`, the stamp of
+    the library this process loaded (pbr_build_info); otherwise (a kernel changed since the profile, or an unstamped
+    profile) they are None and the provenance says so."""
     try:
         with open(path) as f:
             e = json.load(f).get(workload)
@@ -317,7 +350,7 @@ def time_exact_mode(ctx, pc, gb, out, stream, args, fmt, rgba8, px):
             "avg_launch_ms": round(float(np.mean(ms)), 4), "median_launch_ms": round(float(np.median(ms)), 4)}
 
 
-def make_workload(cfg, band, mode: str, device):
+def make_workload(cfg, band, mode: str, device, apply_ao: bool = False):
     """The pass constants, env map and resident G-buffer rows of `band` of frame `cfg` (host fill into
     pinned staging, one upload). Returns (pc, env, staging, gb, fill_s, (first_upload_s, warm_upload_s)).
     The first upload of the process pays the device allocation and the first DMA use of the pinned pages
@@ -329,6 +362,8 @@ def make_workload(cfg, band, mode: str, device):
     pc = S.scene_pass(cfg)
     if mode == "faithful":
         pc.flags = int(pc.flags) | N.PBR_FLAG_FAITHFUL
+    if apply_ao:  # the AO extension (ambient *= AO, PBR_FLAG_APPLY_AO): the kernel reads the AO plane too
+        pc.flags = int(pc.flags) | N.PBR_FLAG_APPLY_AO
     env = S.env_map() if pc.ambient_mode == N.PBR_AMBIENT_IBL_DIFFUSE else None
     staging = torch.empty((N.NUM_PLANES, band.rows, cfg.width), dtype=torch.float32, pin_memory=True)
     S.fill_gbuffer_host(cfg, band.row_begin, band.row_end, out=staging.numpy())
@@ -472,8 +507,22 @@ def main():
                          "to show that a frame off the 1e-5 bar is refused (exit status 3, no metric line)")
     ap.add_argument("--parity-rows", type=int, default=8,
                     help="N > 1: rows per band of the assembled frame checked against the oracle (0 = none)")
+    ap.add_argument("--apply-ao", action="store_true",
+                    help="shade with PBR_FLAG_APPLY_AO (ambient *= AO): the north star's G-buffer AO plane is read "
+                         "(64 B/px, SURVEY 8(d)'s model); the reference itself never reads its AO slot (SURVEY F4), so "
+                         "the default pass does not")
+    ap.add_argument("--dev", action="store_true",
+                    help="measure a library that is not the product build of this checkout (a variant, a debug or stale "
+                         "build, PBR_* overrides): the line is printed with library.problems listed; without --dev such "
+                         "a run exits 4 and prints no metric line")
     args = ap.parse_args()
 
+    # Which binary is measured (pbr_build_info): decided before anything runs, on any host.
+    library = library_provenance(args.dev)
+    if library["problems"] and not args.dev:
+        log("REFUSED: the loaded library is not the product build of this checkout: " + "; ".join(library["problems"]))
+        log("(rebuild with `make -C physically_based_renderer_amd/csrc`, or pass --dev to measure it anyway)")
+        return EXIT_PROVENANCE
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device")
     n_dev = torch.cuda.device_count()
@@ -497,7 +546,7 @@ def main():
     band = D.band_rows(cfg.height, world, rank)
     workload = f"{cfg.name}" + (f"_band{args.rows_per_rank}" if banded else "")
 
-    pc, env, staging, gb, t_fill, t_upload = make_workload(cfg, band, args.mode, device)
+    pc, env, staging, gb, t_fill, t_upload = make_workload(cfg, band, args.mode, device, args.apply_ao)
     ctx = ShadingContext(device.index)
     stream = torch.cuda.current_stream(device)
     ctx.set_pass(pc, stream)
@@ -581,9 +630,12 @@ def main():
         median_kernel_ms = float(np.median(kernel_ms))
         band_px = cfg.width * band.rows
         bpp = bytes_per_pixel(pc, 4 if rgba8 else 16)
+        bpp_read = bytes_read_per_pixel(pc, 4 if rgba8 else 16)
         achieved = bpp * band_px / avg_kernel_s / 1e9
-        traffic, valu_busy, pmc_prov = load_pmc(workload + ("_rgba8" if rgba8 and not banded else "")
-                                                + ("_faithful" if args.mode == "faithful" else ""))
+        traffic, valu_busy, pmc_prov = load_pmc(workload + ("_ao" if pc.flags & N.PBR_FLAG_APPLY_AO else "")
+                                                + ("_rgba8" if rgba8 and not banded else "")
+                                                + ("_faithful" if args.mode == "faithful" else ""),
+                                                library["sources_sha"])
         tile_px = 256 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 128  # culling unit: 32x8 / 64x2
         fpp = flops_per_pixel(pc, cull_note.get("lights_per_tile"), tile_px)
         fpp_exec = executed_flops_per_pixel(pc, stats, band_px)
@@ -595,7 +647,9 @@ def main():
         # that roof is: the VALU. HBM is reported beside it.
         compute_bound = fpp / bpp > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
         hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-               "frac": round(achieved / HBM_PEAK_GBPS, 5)}
+               "frac": round(achieved / HBM_PEAK_GBPS, 5),
+               "bytes_per_px": bpp, "bytes_per_px_read": bpp_read,
+               "achieved_read": round(bpp_read * band_px / avg_kernel_s / 1e9, 2)}
         roofline = {
             "bound": "mfma" if compute_bound else "hbm",
             "achieved": round(tflops, 3) if compute_bound else hbm["achieved"],
@@ -606,7 +660,7 @@ def main():
             "compute_unit": "valu (fp32 vector ALU; no MFMA on this path)" if compute_bound else None,
             "kernel": kernel_name, "avg_launch_ms": round(avg_kernel_s * 1e3, 4),
             "median_launch_ms": round(median_kernel_ms, 4),
-            "flop_per_px": fpp, "bytes_per_px": bpp, "px_per_launch": band_px,
+            "flop_per_px": fpp, "bytes_per_px": bpp, "bytes_per_px_read": bpp_read, "px_per_launch": band_px,
             "executed_flop_per_px": fpp_exec,
             "achieved_executed": round(tflops_exec, 3),
             "frac_executed": round(tflops_exec / FP32_PEAK_TFLOPS, 4),
@@ -665,12 +719,14 @@ def main():
             "warmup": args.warmup, "clock_ramp": ramp,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "output": output, "mode": args.mode,
+            "library": library,
             "data": "synthetic deterministic G-buffer (splitmix64 per pixel; rustediron metal/rough tiles; "
                     "Chelsea_Stairs 16-bit env)",
             "config": {"workload": workload, "width": cfg.width, "height": cfg.height,
                        "rows_per_rank": band.rows, "point_lights": pc.num_point_lights,
                        "ambient": "ibl_diffuse" if pc.ambient_mode else "constant",
                        "tiled_culling": bool(pc.flags & N.PBR_FLAG_TILED_CULLING),
+                       "apply_ao": bool(pc.flags & N.PBR_FLAG_APPLY_AO),
                        "parallelism": f"row-bands x{world}"},
             "hbm_gbps": round(achieved, 2),
             "roofline": roofline,
@@ -678,9 +734,10 @@ def main():
             **parity, **gather_note, **cull_note, **scale,
             **({"exact_mode": exact_leg} if exact_leg is not None else {}),
             # pinned staging -> HBM: the first copy of the process (allocation + first DMA use of the pinned
-            # pages) and the same copy repeated (the link rate); DESIGN.md §6
-            "pcie_h2d_gbps": round(staging.numel() * 4 / t_upload[1] / 1e9, 2),
-            "pcie_h2d_first_gbps": round(staging.numel() * 4 / t_upload[0] / 1e9, 2),
+            # pages; the key's meaning in rounds 1-3 and again from round 5) and the same copy repeated into the
+            # resident buffer (the link rate); DESIGN.md §6
+            "pcie_h2d_gbps": round(staging.numel() * 4 / t_upload[0] / 1e9, 2),
+            "pcie_h2d_warm_gbps": round(staging.numel() * 4 / t_upload[1] / 1e9, 2),
         }
         rc = emit_line(out)
     else:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PBR_ABI_VERSION 8
+#define PBR_ABI_VERSION 9
 #define PBR_MAX_LIGHTS 4096 /* the reference's cbuffer holds MAX_LIGHTS = 16 (LightingUtil.hlsl:7) */
 
 typedef enum pbr_status {
@@ -301,6 +301,13 @@ const char* pbr_strerror(int status);
 /* Last HIP error string recorded by the context (empty if none). */
 const char* pbr_last_error(const pbr_context* ctx);
 int pbr_abi_version(void);
+/* ABI 9: what the library was built from, as JSON: {"abi": 9, "units": [{"unit", "sources_sha", "flavor", "cflags",
+ * "switches": {...}}, ...]} -- one record per compilation unit (pbr_context, shade_kernels, shade_kernels_bal,
+ * gbuffer_fill): the stamp of the sources it was compiled from (sha256 of the csrc sources, the Makefile and this header, first
+ * 16 hex digits), the build flavor ("product" for the Makefile's default target without EXTRA flags; "debug_bounds",
+ * "asan", "custom: ...", "variant: ..." otherwise), its extra compiler flags and every build switch's value. A program
+ * that quotes a measurement can check it ran the product build of a given checkout. Static storage. */
+const char* pbr_build_info(void);
 
 #ifdef __cplusplus
 }

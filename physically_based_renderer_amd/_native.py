@@ -189,6 +189,7 @@ SIGNATURES = {
     "pbr_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "pbr_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "pbr_abi_version": (ctypes.c_int, []),
+    "pbr_build_info": (ctypes.c_char_p, []),
 }
 
 _lib = None
@@ -220,17 +221,55 @@ def lib() -> ctypes.CDLL:
 
 def kernel_sources_sha(csrc_dir: str = CSRC_DIR) -> str:
     """sha256 (first 16 hex digits) of the sources libpbrshade.so is built from (csrc/*.hip, *.h, *.cpp, the
-    Makefile) and the public header: the revision stamp of committed profiles (profiles/pmc_summary.json), so
-    that bench.py quotes counters only when they were measured on the kernels it runs."""
-    import hashlib
+    Makefile) and the public header (_sources.py): the stamp every object of a build carries (build_info) and that
+    committed profiles (profiles/pmc_summary.json) are keyed by."""
+    from ._sources import sources_sha
 
-    h = hashlib.sha256()
-    names = sorted(n for n in os.listdir(csrc_dir) if n.endswith((".hip", ".h", ".cpp")) or n == "Makefile")
-    for path in [os.path.join(csrc_dir, n) for n in names] + [HEADER_PATH]:
-        h.update(os.path.basename(path).encode() + b"\0")
-        with open(path, "rb") as f:
-            h.update(f.read())
-    return h.hexdigest()[:16]
+    return sources_sha(csrc_dir, HEADER_PATH)
+
+
+# The product build: every unit compiled by the Makefile's default target from one checkout (no EXTRA flags, no
+# debug / profiling / experiment switches). Anything else -- the bounds-checked build, an ASan build, a development
+# variant (tools/build_variant.sh), `make EXTRA=...` -- carries another flavor in pbr_build_info.
+PRODUCT_FLAVOR = "product"
+
+
+def build_info() -> dict:
+    """What the LOADED library was built from (pbr_build_info, ABI 9): per compilation unit the sources stamp, the
+    build flavor, its extra compiler flags and the value of every build switch, plus a summary -- `sources_sha` (the
+    units' common stamp, None if they differ), `flavor` (likewise) and `path`. Libraries older than ABI 9 report
+    {"sources_sha": None, "flavor": None, "units": []}."""
+    import json
+
+    handle = lib()
+    if not hasattr(handle, "pbr_build_info"):
+        return {"path": LIB_PATH, "sources_sha": None, "flavor": None, "units": [], "abi": handle.pbr_abi_version()}
+    info = json.loads(handle.pbr_build_info().decode())
+    shas = {u["sources_sha"] for u in info["units"]}
+    flavors = {u["flavor"] for u in info["units"]}
+    info.update(path=os.path.abspath(LIB_PATH), sources_sha=shas.pop() if len(shas) == 1 else None,
+                flavor=flavors.pop() if len(flavors) == 1 else None)
+    return info
+
+
+def build_problems(info: dict = None, tree_sha: str = None) -> list:
+    """Why the loaded library is not provably the product build of this checkout (empty = it is): units compiled
+    from different source states, a stamp other than the checkout's, or a non-product flavor (debug, profiling,
+    experiment or EXTRA flags)."""
+    info = build_info() if info is None else info
+    tree_sha = kernel_sources_sha() if tree_sha is None else tree_sha
+    bad = []
+    if not info["units"]:
+        return ["the library reports no build info (ABI < 9)"]
+    if info["sources_sha"] is None:
+        bad.append("units built from different sources: " + ", ".join(f"{u['unit']}={u['sources_sha']}"
+                                                                       for u in info["units"]))
+    elif info["sources_sha"] != tree_sha:
+        bad.append(f"library built from sources {info['sources_sha']}, checkout is {tree_sha}")
+    for u in info["units"]:
+        if u["flavor"] != PRODUCT_FLAVOR:
+            bad.append(f"unit {u['unit']} is a {u['flavor']!r} build")
+    return bad
 
 
 def status_string(status: int) -> str:

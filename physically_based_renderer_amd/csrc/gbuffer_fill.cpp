@@ -465,3 +465,8 @@ extern "C" int pbr_scene_pass(const pbr_scene_desc* scene, int32_t n_lights, pbr
     }
     return PBR_OK;
 }
+
+// This unit's build record (pbr_build_info.h, pbr_build_info).
+#include "pbr_build_info.h"
+extern "C" __attribute__((used, visibility("default"))) const char pbr_unit_info_gbuffer_fill[] =
+    PBR_UNIT_INFO("gbuffer_fill", "");

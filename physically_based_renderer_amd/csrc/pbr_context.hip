@@ -14,6 +14,17 @@
 #include "pbr/pbr_shade.h"
 #include "shade_kernels.h"
 #include "pbr_debug_bounds.h"
+#include "pbr_build_info.h"
+
+// The build records of the library's units (pbr_build_info.h). Weak: a profiling build compiles the balanced kernels
+// into shade_kernels.hip's unit, so shade_kernels_bal's record is then absent (null) and not listed.
+extern "C" {
+extern const char pbr_unit_info_shade_kernels[] __attribute__((weak));
+extern const char pbr_unit_info_shade_kernels_bal[] __attribute__((weak));
+extern const char pbr_unit_info_gbuffer_fill[] __attribute__((weak));
+__attribute__((used)) const char pbr_unit_info_pbr_context[] =
+    PBR_UNIT_INFO("pbr_context", PBR_BI_SWITCH(PBR_DEBUG_BOUNDS));
+}
 
 // Cross-stream ordering of the context's device resources (the reference's 3-deep FrameResource ring,
 // FrameResource.h:111-140, PBRApp.cpp:220-243, is the same idea on D3D12 fences). A resource -- a light slot,
@@ -206,18 +217,17 @@ hipError_t before_write(pbr_context* ctx, Resource& r, hipStream_t w, int wi) {
     return hipSuccess;
 }
 
-// Wait on the host for every reader of `r` (before freeing its memory). The readers' streams are synchronised
-// themselves: a context used from one stream records no per-pass event, so an event wait would return at once.
+// Wait on the host for every reader and the writer of `r` (before freeing its memory). Growing a resource is rare, so
+// this synchronises the device: every queued pass that may read `r`, on whatever stream, and its upload are then
+// complete, and no other resource has a pending reader either. It never touches the readers' stream handles, which
+// the caller may have destroyed after their passes finished (or a new stream may have reused): synchronising such a
+// handle failed or waited on an unrelated stream. (A per-pass event of the reader would not do: a context used from
+// one stream records none.)
 hipError_t before_free(pbr_context* ctx, Resource& r) {
-    for (int i : r.readers) {
-        const hipError_t e = hipStreamSynchronize(ctx->streams[i].stream);
-        if (e != hipSuccess) return e;
-    }
-    r.readers.clear();
-    if (r.writer >= 0 && r.written) {
-        const hipError_t e = hipEventSynchronize(r.written);
-        if (e != hipSuccess) return e;
-    }
+    if (r.readers.empty() && r.writer < 0) return hipSuccess;
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    forget_readers(ctx);
     return hipSuccess;
 }
 
@@ -260,6 +270,22 @@ void forget_readers(pbr_context* ctx) {
 extern "C" {
 
 int pbr_abi_version(void) { return PBR_ABI_VERSION; }
+
+const char* pbr_build_info(void) {
+    static const std::string info = [] {
+        std::string r = "{\"abi\": " + std::to_string(PBR_ABI_VERSION) + ", \"units\": [";
+        bool first = true;
+        for (const char* u : {pbr_unit_info_pbr_context, pbr_unit_info_shade_kernels, pbr_unit_info_shade_kernels_bal,
+                              pbr_unit_info_gbuffer_fill}) {
+            if (u == nullptr) continue;
+            r += first ? "" : ", ";
+            r += u;
+            first = false;
+        }
+        return r + "]}";
+    }();
+    return info.c_str();
+}
 
 const char* pbr_strerror(int status) {
     switch (status) {

@@ -77,8 +77,19 @@ constexpr int kTileW = 64;  // pixels; 32 work-items x 2 pixels
 #define PBR_X2_MIN_WAVES 4  // waves per SIMD the packed kernel is register-allocated for
 #endif
 #ifndef PBR_LEAN_MIN_WAVES
-#define PBR_LEAN_MIN_WAVES 4  // waves per SIMD the lean pair kernel is register-allocated for
+#define PBR_LEAN_MIN_WAVES 4  // waves per SIMD the culled lean pair kernel is register-allocated for
 #endif
+#ifndef PBR_LEAN_UNIFORM_MIN_WAVES
+#define PBR_LEAN_UNIFORM_MIN_WAVES 5  // ... and the unculled (uniform-loop) faithful or constant-ambient ones
+#endif
+// Waves per SIMD of shade_lean_kernel<AMBIENT, .., CULL, FAITHFUL>: five for the uniform loops, whose loads wait on HBM
+// latency with too few waves to cover it (config 2: DESIGN.md §5d), where 96 VGPRs hold the loop without scratch (the
+// faithful ones park albedo and 1 - metallic in LDS across it, lean_wave); four for the culled loops (the culled walk
+// and its survivor masks need ~105-116 VGPRs) and for the exact diffuse-IBL loop (20 B/lane of scratch at 96).
+template <int AMBIENT, bool CULL, bool FAITHFUL>
+constexpr int lean_min_waves() {
+    return CULL || (!FAITHFUL && AMBIENT == kAmbientIblDiffuse) ? PBR_LEAN_MIN_WAVES : PBR_LEAN_UNIFORM_MIN_WAVES;
+}
 constexpr int kTileH = 8;
 constexpr int kBlock = 256;
 constexpr int kChunk = 256;  // lights staged per LDS pass
@@ -1127,6 +1138,7 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         return;
     }
     const int64_t row = (int64_t)y * gb.row_stride;
+    __shared__ v2 s_park[4][64];   // uniform-loop faithful waves: albedo, 1 - metallic across the light loop
     bool need_a, need_b;           // pixels for the IEEE path (the exact re-pass)
     bool faithful_wave = false;    // wave-uniform
     int kept_total = 0;
@@ -1177,12 +1189,30 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         f3x2 d2;
         if (faithful_wave) {
             if (!CULL) faithful_scale(q2);
+            // Uniform-loop (5-wave) kernels: albedo and 1 - metallic feed the faithful loop only through make_faithful's
+            // hoisted products, but the finish needs them; parked in LDS across the loop (the memory clobber keeps the
+            // compiler from forwarding the stored values), they hold no VGPRs there: at the 96-VGPR budget of five
+            // waves per SIMD the loop then runs without scratch.
+            if constexpr (!CULL) {
+                const int l = (int)(threadIdx.x & 63);
+                s_park[0][l] = q2.albedo.x;
+                s_park[1][l] = q2.albedo.y;
+                s_park[2][l] = q2.albedo.z;
+                s_park[3][l] = q2.one_minus_metal;
+                asm volatile("" ::: "memory");
+            }
             if (lean_wave)
                 d2 = lighting_fast<CULL, true, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total,
                                                      nullptr, nullptr, false, false, BalMasks{}, nullptr, &first);
             else
                 d2 = lighting_fast<CULL, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total,
                                                       nullptr, nullptr, false, false, BalMasks{}, nullptr, &first);
+            if constexpr (!CULL) {
+                asm volatile("" ::: "memory");
+                const int l = lane_id_fresh();
+                q2.albedo = f3x2{s_park[0][l], s_park[1][l], s_park[2][l]};
+                q2.one_minus_metal = s_park[3][l];
+            }
             if (!CULL) faithful_unscale(q2);
         } else if (lean_wave) {
             d2 = lighting_fast<CULL, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
@@ -1249,7 +1279,7 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
 // persistent grid of 3 or 4 waves per SIMD walking the waves (same-box A/B config 2 0.058 -> 0.090 ms: each wave
 // then waits for its own G-buffer loads, which the independent waves overlap).
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, bool FAITHFUL>
-__global__ __launch_bounds__(64, PBR_LEAN_MIN_WAVES) void shade_lean_kernel(GBufferArgs gb, PassArgs ps,
+__global__ __launch_bounds__(64, (lean_min_waves<AMBIENT, CULL, FAITHFUL>())) void shade_lean_kernel(GBufferArgs gb, PassArgs ps,
                                                             const float4* __restrict__ lights,
                                                             const float4* __restrict__ env, FrameArgs fr,
                                                             int32_t* __restrict__ tile_kept) {
@@ -1598,3 +1628,21 @@ hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels,
 #endif  // !PBR_BAL_TU
 
 }  // namespace pbr
+
+// This unit's build record (pbr_build_info.h, pbr_build_info): the stamp, flavor and flags it was compiled with and
+// every build switch of the kernels as the preprocessor saw it.
+#include "pbr_build_info.h"
+#define PBR_KERNEL_SWITCHES                                                                                        \
+    PBR_BI_SWITCH(PBR_X2_MIN_WAVES) ", " PBR_BI_SWITCH(PBR_LEAN_MIN_WAVES) ", " PBR_BI_SWITCH(PBR_LEAN_UNIFORM_MIN_WAVES) \
+    ", " PBR_BI_SWITCH(PBR_BAL_PROFILE) ", " \
+    PBR_BI_SWITCH(PBR_WAVE_TIMELINE) ", " PBR_BI_SWITCH(PBR_DEBUG_BOUNDS) ", " PBR_BI_SWITCH(PBR_SPLIT_BAL) ", "   \
+    PBR_BI_SWITCH(PBR_POW5_LDS) ", " PBR_BI_SWITCH(PBR_POW5_GLIBC_FROM) ", "                                     \
+    PBR_BI_SWITCH(PBR_POW5_FAST3_GLIBC_FROM) ", " PBR_BI_SWITCH(PBR_FAITHFUL_GAMMA_LO) ", "                      \
+    PBR_BI_SWITCH(PBR_ATAN2F_KMAX)
+#if PBR_BAL_TU
+extern "C" __attribute__((used, visibility("default"))) const char pbr_unit_info_shade_kernels_bal[] =
+    PBR_UNIT_INFO("shade_kernels_bal", PBR_KERNEL_SWITCHES);
+#else
+extern "C" __attribute__((used, visibility("default"))) const char pbr_unit_info_shade_kernels[] =
+    PBR_UNIT_INFO("shade_kernels", PBR_KERNEL_SWITCHES);
+#endif

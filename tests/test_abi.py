@@ -20,7 +20,7 @@ def test_library_loads_and_exports_every_header_symbol():
         assert hasattr(lib, name), f"{name} declared in pbr_shade.h but not exported"
         assert name in N.SIGNATURES, f"{name} has no ctypes signature"
     assert set(N.SIGNATURES) == set(declared)
-    assert lib.pbr_abi_version() == 8
+    assert lib.pbr_abi_version() == 9
 
 
 def test_exports_are_c_symbols():
@@ -100,7 +100,7 @@ def test_bounds_checked_build_loads_and_exports_the_abi():
         pytest.skip("bounds-checked build not built (make -C physically_based_renderer_amd/csrc debug-bounds)")
     code = ("from physically_based_renderer_amd import _native as N; L = N.lib(); "
             "missing = [s for s in N.header_symbols() if not hasattr(L, s)]; "
-            "assert not missing, missing; assert L.pbr_abi_version() == 8; "
+            "assert not missing, missing; assert L.pbr_abi_version() == 9; "
             "assert L.pbr_debug_bounds(None, None, 0) == -1; print('ok')")
     r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "PBR_LIB_PATH": dbg}, capture_output=True,
                        text=True, timeout=120, cwd=ROOT)

@@ -13,13 +13,21 @@ from physically_based_renderer_amd import _native as N
 from physically_based_renderer_amd import scenes as S
 
 
-def test_bytes_per_pixel_follows_the_planes_read():
+def test_bytes_per_pixel_model_and_reads():
+    """SURVEY 8(d)'s algorithmic bytes (the roofline figure) beside what the kernel reads: 8(d) counts the AO plane of
+    the north star's G-buffer, which the reference never reads and the kernel reads only with
+    PBR_FLAG_APPLY_AO."""
     pc3 = S.scene_pass(S.CONFIGS[3])
-    assert bench.bytes_per_pixel(pc3) == 60            # 11 planes + RGBA fp32
-    assert bench.bytes_per_pixel(pc3, 4) == 48         # RGBA8 back buffer
+    assert bench.bytes_per_pixel(pc3) == 64            # 12 planes + RGBA fp32 (8(d): configs 1-3, 5)
+    assert bench.bytes_per_pixel(pc3, 4) == 52         # RGBA8 back buffer
+    assert bench.bytes_read_per_pixel(pc3) == 60       # 11 planes read
+    assert bench.bytes_read_per_pixel(pc3, 4) == 48
+    pc3.flags = int(pc3.flags) | N.PBR_FLAG_APPLY_AO
+    assert bench.bytes_read_per_pixel(pc3) == bench.bytes_per_pixel(pc3) == 64
     pc4 = S.scene_pass(S.CONFIGS[4])
     assert pc4.flags & N.PBR_FLAG_F0_PLANE
-    assert bench.bytes_per_pixel(pc4) == 72            # + F0 plane
+    assert bench.bytes_per_pixel(pc4) == 76            # + F0 plane (8(d): config 4)
+    assert bench.bytes_read_per_pixel(pc4) == 72
 
 
 def test_flops_per_pixel_and_the_roof():
@@ -43,7 +51,7 @@ def test_pmc_lookup_is_keyed_by_workload_and_mode(tmp_path):
     for key in ("cfg3_3840x2160_64pt_ibl_chelsea", "cfg3_3840x2160_64pt_ibl_chelsea_faithful"):
         assert key in summary
         e = summary[key]
-        traffic, busy, prov = bench.load_pmc(key)
+        traffic, busy, prov = bench.load_pmc(key, head)
         assert prov["kernel_sources_sha"] == head
         if e.get("kernel_sources_sha") == head:  # profiled at this revision of the kernels: quoted
             assert traffic == e["hbm_bytes_per_launch"] and 0.5 < busy <= 1.0 and "stale" not in prov
@@ -55,14 +63,14 @@ def test_pmc_lookup_is_keyed_by_workload_and_mode(tmp_path):
         # the committed kernel trace agrees with the bench's own events within 2 %
         kt = e["kernel_trace"]
         assert abs(kt["mean_ms_timed_steps"] - kt["bench_avg_launch_ms"]) / kt["bench_avg_launch_ms"] < 0.02
-    assert bench.load_pmc("no_such_workload")[:2] == (None, None)
+    assert bench.load_pmc("no_such_workload", head)[:2] == (None, None)
     # the stamp decides: the same entry quoted under this build's hash, refused under another
     e = dict(summary["cfg3_3840x2160_64pt_ibl_chelsea_faithful"])
     for sha, quoted in ((head, True), ("0" * 16, False)):
         e["kernel_sources_sha"] = sha
         p = tmp_path / f"s_{sha}.json"
         p.write_text(json.dumps({"w": e}))
-        traffic, busy, prov = bench.load_pmc("w", str(p))
+        traffic, busy, prov = bench.load_pmc("w", head, str(p))
         assert (traffic == e["hbm_bytes_per_launch"]) if quoted else (traffic is None and prov["stale"])
 
 

@@ -221,3 +221,47 @@ def test_last_pass_kernel_names_the_launched_kernel():
             ctx.shade(GBuffer.from_host(planes, dev))
             torch.cuda.synchronize()
             assert ctx.last_kernel() == want, (cid, flags)
+
+
+@pytest.mark.parametrize("first", ["lights", "env"])
+def test_grow_resources_after_a_reader_stream_is_destroyed(first, gpu, env_map):
+    """A pass on a caller-created stream S, S destroyed once its passes finished (the contract, pbr_shade.h), then
+    the context's resources grow past their capacity -- more lights than the slot S read held (the ring's four slots
+    cycled back to it), a larger environment map: the frees before the growth must not touch S's dead handle
+    (pbr_context.hip before_free synchronises the device instead), and the next pass carries the bits of the same
+    pass on a fresh context. `first`: which resource grows first (the first growth meets S's record)."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    cfg = S.CONFIGS[3].with_size(256, 64)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    gb = GBuffer.from_host(planes, gpu)
+    pc = S.scene_pass(cfg)
+    rng = np.random.default_rng(3)
+    more = np.concatenate([pc.light_array()] * 3)[:150].copy()  # 150 lights: past the slot's 64
+    more[:, 8:11] = rng.uniform(-20, 20, (150, 3))
+    pc_big = _with(pc, num_point_lights=150, lights_array=more)
+    env_big = np.ascontiguousarray(np.tile(env_map, (2, 2, 1)))  # 4x the texels of the first map
+    with ShadingContext(0) as ctx:
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        ctx.set_pass(pc, stream=s.value)  # slot 0
+        ctx.set_env_map(env_map, stream=s.value)
+        ctx.shade(gb, stream=s.value)
+        ctx.shade(gb)  # a second stream: the context now tracks both
+        assert hip.hipStreamSynchronize(s) == 0
+        assert hip.hipStreamDestroy(s) == 0
+        for _ in range(3):  # slots 1-3; the next pbr_set_pass reuses slot 0
+            ctx.set_pass(pc)
+        if first == "lights":
+            ctx.set_pass(pc_big)  # grows slot 0, which S read
+            ctx.set_env_map(env_big)
+        else:
+            ctx.set_env_map(env_big)  # grows the texture S read
+            ctx.set_pass(pc_big)
+        got = ctx.shade(gb)
+        torch.cuda.synchronize()
+        got = got.cpu().numpy()
+    with ShadingContext(0) as fresh:
+        want, _ = _solo(fresh, gb, pc_big, env_big)
+    assert O.bit_equal(got, want).all()

@@ -33,12 +33,17 @@ def test_pmc_counters_average_the_workloads_own_dispatches(tmp_path):
     assert pmc.per_kernel(str(path)) == {"FETCH_SIZE": 100.0}
 
 
-def test_profiled_tree_stamp(tmp_path, monkeypatch):
-    """PBR_PROFILED_TREE stamps a summary with the sources of the tree that was profiled."""
-    pmc = load_tool("pmc_summarize")
-    from physically_based_renderer_amd import _native as N
+def test_profile_stamp_comes_from_the_loaded_library():
+    """A profile is stamped with the library the profiled bench process loaded (its line's `library`, pbr_build_info),
+    and a development / debug / stale build is refused rather than stamped."""
+    import pytest
 
-    monkeypatch.delenv("PBR_PROFILED_TREE", raising=False)
-    assert pmc.profiled_sources_sha() == N.kernel_sources_sha()
-    monkeypatch.setenv("PBR_PROFILED_TREE", ROOT)
-    assert pmc.profiled_sources_sha() == N.kernel_sources_sha()
+    pmc = load_tool("pmc_summarize")
+    lib = {"path": "physically_based_renderer_amd/_lib/libpbrshade.so", "sources_sha": "abcd" * 4, "flavor": "product",
+           "tree_sources_sha": "abcd" * 4, "problems": []}
+    sha, rec = pmc.library_stamp({"library": lib})
+    assert sha == "abcd" * 4 and rec["flavor"] == "product"
+    for bad in ({"library": {**lib, "problems": ["unit shade_kernels_bal is a 'variant: x' build"]}},
+                {"library": {**lib, "sources_sha": None}}, {}, None):
+        with pytest.raises(SystemExit):
+            pmc.library_stamp(bad)

@@ -5,8 +5,9 @@ that bench.py reads for roofline.traffic.
 HBM bytes per launch = FETCH_SIZE x 2 + WRITE_SIZE (KiB; gfx950 FETCH_SIZE reports half of a
 coalesced read, MI355X_MICROARCH.md "HBM"), averaged over the shading kernel's dispatches.
 usage: python tools/pmc_summarize.py <tag> <workload> <pixels> <bytes_per_px> <lights> <revision> [<profiles subdir>]
-The kernel_sources_sha stamp is computed from this checkout, or, with PBR_PROFILED_TREE=<dir>, from a checkout of
-the profiled revision (a git worktree) when the sources have moved on since the run.
+The entry's kernel_sources_sha is the stamp of the library the PROFILED process loaded (the bench line's `library`,
+pbr_build_info): a profile of a development, debug or stale build (library.problems non-empty) is refused, and the
+stamp never comes from the files of the checkout that summarises it.
 """
 import csv
 import glob
@@ -17,21 +18,19 @@ import sys
 
 N_SIMD = 256 * 4  # MI355X: 256 CUs x 4 SIMDs
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
-from physically_based_renderer_amd._native import kernel_sources_sha  # noqa: E402
+# Entry fields that are not measurements and survive a re-profile of the same library (anything else is replaced).
+CARRIED = ("note",)
 
 
-def profiled_sources_sha():
-    tree = os.environ.get("PBR_PROFILED_TREE")
-    if not tree:
-        return kernel_sources_sha()
-    import physically_based_renderer_amd._native as nat
-    saved = nat.HEADER_PATH
-    nat.HEADER_PATH = os.path.join(tree, "include", "pbr", "pbr_shade.h")
-    try:
-        return kernel_sources_sha(os.path.join(tree, "physically_based_renderer_amd", "csrc"))
-    finally:
-        nat.HEADER_PATH = saved
+def library_stamp(bench_line: dict) -> tuple:
+    """(sources stamp, library record) of the library the profiled bench process loaded; raises SystemExit when that
+    was not the product build of its checkout, or when the line predates pbr_build_info."""
+    lib = (bench_line or {}).get("library")
+    if not lib or not lib.get("sources_sha"):
+        raise SystemExit("the profiled bench line names no library build (pbr_build_info): cannot stamp the profile")
+    if lib.get("problems"):
+        raise SystemExit("the profiled library is not a product build: " + "; ".join(lib["problems"]))
+    return lib["sources_sha"], {k: lib[k] for k in ("path", "sources_sha", "flavor", "tree_sources_sha") if k in lib}
 
 
 def find(pattern):
@@ -71,6 +70,11 @@ def main():
         p = find(f"{src}/pmc_{name}/**/*counter_collection.csv")
         shutil.copy(p, os.path.join(dst, f"pmc_{name}_{workload}.csv"))
         counters.update(per_kernel(p))
+    bench = None
+    for line in open(os.path.join(src, "kt.log")):
+        if line.startswith("{"):
+            bench = json.loads(line)
+    stamp, library = library_stamp(bench)
     hbm = counters["FETCH_SIZE"] * 2 * 1024 + counters["WRITE_SIZE"] * 1024
     alg = pixels * bpp
     entry = {
@@ -88,8 +92,12 @@ def main():
         "valu_issue_busy": counters["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD / (counters["GRBM_GUI_ACTIVE"] / 8),
         "source": f"profiles/{dst_tag}/pmc_*_{workload}.csv (rocprofv3 --pmc, separate passes, bench.py --steps 5)",
         "kernel_revision": revision,
-        # bench.py quotes traffic / valu_issue_busy only while the kernel sources still hash to this
-        "kernel_sources_sha": profiled_sources_sha(),
+        # bench.py quotes traffic / valu_issue_busy only while the library it loads carries this stamp
+        "kernel_sources_sha": stamp,
+        "library": library,
+        "kernel": bench["roofline"].get("kernel"),
+        # the balanced exact kernel reads the G-buffer pair again after its light loop (+44 B/px)
+        "pair_reread": str(bench["roofline"].get("kernel", "")).endswith(", 2>"),
     }
     # Kernel trace of the bench run itself: mean launch time over the timed steps (the last K launches;
     # the clock-ramp and warm-up launches come first) next to the bench's own HIP-event average.
@@ -98,10 +106,6 @@ def main():
     with open(trace) as f:
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in csv.DictReader(f)
                 if "shade_tile" in r["Kernel_Name"] or "shade_lean" in r["Kernel_Name"]]
-    bench = None
-    for line in open(os.path.join(src, "kt.log")):
-        if line.startswith("{"):
-            bench = json.loads(line)
     # launch order of bench.py: clock ramp, warm-up steps, the K timed steps, then (exact leg, scale anchor)
     k = bench["steps"] if bench else len(durs)
     first = bench["clock_ramp"]["launches"] + bench["warmup"] if bench else len(durs) - k
@@ -114,8 +118,11 @@ def main():
     }
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     summary = json.load(open(path)) if os.path.exists(path) else {}
-    for k, v in summary.get(workload, {}).items():  # hand-written annotations (e.g. pair_reread) survive a re-profile
-        entry.setdefault(k, v)
+    old = summary.get(workload, {})
+    if old.get("kernel_sources_sha") == stamp:  # hand-written notes survive a re-profile of the same library only
+        for k in CARRIED:
+            if k in old:
+                entry.setdefault(k, old[k])
     summary[workload] = entry
     json.dump(summary, open(path, "w"), indent=1)
     print(json.dumps(entry, indent=1))
