@@ -78,7 +78,8 @@ enum pbr_pass_flags {
                                          attenuation) use the hardware reciprocal (<= 1 ulp) instead of
                                          correct rounding; the ill-conditioned GGX chain and Fresnel stay
                                          exact. Output within 1e-5 relative of the reference evaluation
-                                         (the north-star bar; bound 6.1e-6, tiled passes 6.4e-6; measured 6.3e-7), not bit-identical.
+                                         (the north-star bar; bound 6.1e-6, tiled and wave-balanced passes
+                                         6.4e-6; measured 6.3e-7), not bit-identical.
                                          Applies where every light term is >= 0 and the sum is short:
                                          <= 64 lights (with PBR_FLAG_TILED_CULLING: <= 64 surviving lights,
                                          counted per wave), non-negative strengths, ambient and env texels

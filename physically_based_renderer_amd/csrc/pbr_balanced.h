@@ -36,9 +36,9 @@
 // F stay finite and G = 0. The pixel on the light (l = 0: L = 0 / 0 = NaN) is the same case. Every other
 // factor is finite for a pixel and light inside the fast-path window (the lean-wave bounds of brdf_x2: den in
 // [2^-37, PI], F0 window; attenuation <= 1e4). So every skipped term is +-0 in the reference and needs no
-// window test; live items run the usual window tests (the plain loop also sends pixels with |V + L| < 2^-30
-// or a light closer than 0.01 to the exact re-pass for such items; here that happens only when the item is
-// live). Lights whose fast-path flag is off (pbr_set_pass) make the host choose the uniform loop
+// window test; live items run the |V + L| >= 2^-30 test in pass 2, and their distance window (a light closer than
+// 0.01, 2^-20 in exact mode) is decided in pass 1 (balanced_pass1: near_a / near_b), so either sends the pixel to the
+// exact re-pass as the plain loop would, here only when the item is live. Lights whose fast-path flag is off (pbr_set_pass) make the host choose the uniform loop
 // (PassArgs::balanced), which sends every pixel to the exact re-pass.
 #pragma once
 #include <cstdint>
@@ -77,8 +77,8 @@ __device__ unsigned long long* g_bal_prof_buf;  // 16 per wave, wave = block * 4
 // off) and entry kBalMaxLights is the sentinel of pass 2 (an iteration's second element when one light is left, both
 // elements of a lane with none): strength 0, so its term is (finite) * 0 = +-0, at the position kBalSentinelPos = 2^24
 // on each axis, more than 2.7e7 units from any pixel of the fast window (|P| <= 2^20 per component; the distance, its
-// square and the attenuation stay inside the fast division / sqrt windows), so its window tests (dist >= 0.01,
-// |V + L| >= 2^-30) pass unless V is within ~2^-30 of the direction away from that point: a sentinel item no longer
+// square and the attenuation stay inside the fast division / sqrt windows), so its window test (|V + L| >= 2^-30;
+// it is never a live light of pass 1's distance window) passes unless V is within ~2^-30 of the direction away from that point: a sentinel item no longer
 // sends a live pixel to the exact re-pass (at position 0 it did for every pixel within 0.01 of the origin).
 constexpr int kBalLdsStride = kBalMaxLights + 4;  // 68 floats: every array 16-byte aligned
 constexpr float kBalSentinelPos = 0x1p24f;
@@ -260,15 +260,29 @@ __device__ __forceinline__ float bal_wave_max(float v) {
     return v;
 }
 
-// Pass 1 for the pair and one light (position lx, ly, lz): shift the light's SKIP bit for each pixel (the sign of
-// t1, see the header comment) into `ma` / `mb` (bit 31 after this call). kb = c |N|_1 B - N.P per pixel, with the
-// wave's bound B = max_j B_j (any B >= B_j keeps the skip proof: the margin term only grows), so the test is three
-// FMAs per pixel and light.
-__device__ __forceinline__ void push_skip_bits(uint32_t& ma, uint32_t& mb, float lx, float ly, float lz,
-                                               const f3x2& n, v2 kb) {
-    const v2 t1 = vfma(n.x, splat(lx), vfma(n.y, splat(ly), vfma(n.z, splat(lz), kb)));
-    ma = __builtin_amdgcn_alignbit(ma, __float_as_uint(t1.x), 31);  // (m << 1) | sign(t1)
-    mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(t1.y), 31);
+// Pass 1 for the pair and four lights j..j+3 (coordinates x, y, z: one float4 per axis, light j + i in element i):
+// shift the lights' SKIP bits for each pixel (the sign of t1, see the header comment) into `ma` / `mb`, light j + 3
+// first, so that light j ends lowest. kb = c |N|_1 B - N.P per pixel, with the wave's bound B = max_j B_j (any B >= B_j
+// keeps the skip proof: the margin term only grows), so the test is three FMAs per pixel and light:
+// t1 = N.x l.x + (N.y l.y + (N.z l.z + kb)). Each packed FMA takes two LIGHTS of one pixel (the light pairs are the
+// quads' aligned halves, the pixel's values splat operands of the loop-invariant pixel pair): the earlier form (two
+// pixels, one light splat from the quad) overwrote quads it still had to splat from, which cost ~0.9 moves per light.
+__device__ __forceinline__ void push_skip_bits4(uint32_t& ma, uint32_t& mb, float4 x, float4 y, float4 z,
+                                                const f3x2& n, v2 kb) {
+    const v2 x01 = v2{x.x, x.y}, x23 = v2{x.z, x.w}, y01 = v2{y.x, y.y}, y23 = v2{y.z, y.w};
+    const v2 z01 = v2{z.x, z.y}, z23 = v2{z.z, z.w};
+    const v2 ta01 = vfma(splat(n.x.x), x01, vfma(splat(n.y.x), y01, vfma(splat(n.z.x), z01, splat(kb.x))));
+    const v2 ta23 = vfma(splat(n.x.x), x23, vfma(splat(n.y.x), y23, vfma(splat(n.z.x), z23, splat(kb.x))));
+    const v2 tb01 = vfma(splat(n.x.y), x01, vfma(splat(n.y.y), y01, vfma(splat(n.z.y), z01, splat(kb.y))));
+    const v2 tb23 = vfma(splat(n.x.y), x23, vfma(splat(n.y.y), y23, vfma(splat(n.z.y), z23, splat(kb.y))));
+    ma = __builtin_amdgcn_alignbit(ma, __float_as_uint(ta23.y), 31);  // (m << 1) | sign(t1)
+    mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(tb23.y), 31);
+    ma = __builtin_amdgcn_alignbit(ma, __float_as_uint(ta23.x), 31);
+    mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(tb23.x), 31);
+    ma = __builtin_amdgcn_alignbit(ma, __float_as_uint(ta01.y), 31);
+    mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(tb01.y), 31);
+    ma = __builtin_amdgcn_alignbit(ma, __float_as_uint(ta01.x), 31);
+    mb = __builtin_amdgcn_alignbit(mb, __float_as_uint(tb01.x), 31);
 }
 
 // Pass 2's light records for one iteration (element 0: light j0; element 1: light j1; index kBalMaxLights is the
@@ -316,8 +330,7 @@ __device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0
 __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const f3x2& lp, const f3x2& ls, m2& ok,
                                                       f3x2& sum, uint64_t live) {
     f3x2 l = f3x2{lp.x - q.pos.x, lp.y - q.pos.y, lp.z - q.pos.z};
-    const v2 dist = sqrt_nr(dot3(l, l));
-    ok &= ge(dist, 0.01f);
+    const v2 dist = sqrt_nr(dot3(l, l));  // >= 0.01 for a live item of a pixel pass 1 did not redo
     const Recip2 rdist = recip_nr(dist);
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     const f3x2 h = normalize_x2(f3x2{q.v.x + l.x, q.v.y + l.y, q.v.z + l.z}, ok);
@@ -357,8 +370,7 @@ __device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3
     q.four_n_dot_v = splat(p.nv4);
     q.f0_nonzero = m2{~0ull, ~0ull};  // not read by the lean BRDF
     f3x2 l = f3x2{lp.x - p.pos.x, lp.y - p.pos.y, lp.z - p.pos.z};
-    const v2 dist = sqrt_nr(dot3(l, l));
-    ok &= ge(dist, 0x1p-20f);
+    const v2 dist = sqrt_nr(dot3(l, l));  // >= 2^-20 (kBalDistLoExact) unless pass 1 redoes the pixel
     const Recip2 rdist = recip_nr(dist);
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
     const f3x2 h = normalize_x2(add3(q.v, l), ok);
@@ -370,7 +382,13 @@ __device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3
 // The live-light masks of the pair's pixels (pass 1), light j at bit j % 32 of word j / 32.
 struct BalMasks {
     uint32_t a0, a1, c0, c1;  // pixel a: lights [0, 32), [32, 64); pixel b: the same
+    bool near_a, near_b;      // the pixel has a live light closer than the distance window (pass 1): redo it
 };
+
+// The distance windows of the two item forms (the lean loops' `ge(dist, lo)` of point_or_spot_faithful_x2 and
+// point_or_spot_x2), decided in pass 1 instead of per item.
+constexpr float kBalDistLoFaithful = 0.01f;
+constexpr float kBalDistLoExact = 0x1p-20f;
 
 // The reference's range cut (LightingUtil.hlsl:129-131: d = length(lightVec); if (d > 100) return 0) as pass 1 applies it
 // to a light whose range boundary crosses the wave's box: d = RN(sqrt(x)) with x = dot(l, l) in HLSL order (the kernel's
@@ -390,8 +408,13 @@ __device__ __forceinline__ m2 beyond_range(const f3x2& pos, float lx, float ly, 
 // no range test: a light farther than 100 from every pixel of the wave's box is dropped for the wave (its terms are
 // the +0 the reference adds); a light whose range boundary crosses the box is tested per pixel (beyond_range, the
 // reference's own decision), a light within 99.9 of every corner is kept as the back-face test says.
+// The distance window of pass 2's items (dist >= dist_lo, kBalDistLo*) is decided here as well: a light whose box
+// distance proves it (the nearest box point at least 1.02 dist_lo away: every pixel's dist >= dist_lo after the few
+// roundings) needs no test; for another (rare) light each pixel whose live mask holds it runs the item's own test --
+// the same dist from the same operations -- and a pixel that fails is redone on the exact path (near_a / near_b), as
+// a failed window test in pass 2 would have redone it.
 __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& n, bool live_a, bool live_b, int nl,
-                                                   BalancedWaveLds& w, const float* lds_lights,
+                                                   float dist_lo, BalancedWaveLds& w, const float* lds_lights,
                                                    unsigned long long* bal_prof = nullptr) {
     const int lane_id = (int)(threadIdx.x & 63);
     BAL_PROF_T(t0);
@@ -414,6 +437,7 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
                                           live_b ? (fabsf(pb.x) + fabsf(pb.y)) + fabsf(pb.z) : 0.0f));
     float bj = 0.0f;  // B_j of light j = lane (j < nl; padded lights: zero position, harmless), B = the maximum
     bool near = true, far = false;  // light j: within range of every pixel of the box / beyond range of every one
+    bool close = false;             // light j may come closer than dist_lo to a pixel of the box (or is NaN)
     if (lane_id < nl) {
         const float lx = lds_lights[lane_id], ly = lds_lights[kBalLdsStride + lane_id],
                     lz = lds_lights[2 * kBalLdsStride + lane_id];
@@ -430,9 +454,10 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
                     gz = fmaxf(fmaxf(mnz - lz, lz - mxz), 0.0f);
         near = (fx * fx + fy * fy) + fz * fz <= 99.9f * 99.9f;
         far = (gx * gx + gy * gy) + gz * gz >= 100.1f * 100.1f;
+        close = !((gx * gx + gy * gy) + gz * gz >= (1.02f * dist_lo) * (1.02f * dist_lo));
     }
     const float bmax = bal_wave_max(bj);
-    const uint64_t far_m = lanes(far), cross_m = lanes(!near && !far);  // bit j: light j (lane j)
+    const uint64_t far_m = lanes(far), cross_m = lanes(!near && !far), close_m = lanes(close);  // bit j: light j
     const v2 cn = v2{0x1p-18f * ((fabsf(n.x.x) + fabsf(n.y.x)) + fabsf(n.z.x)),
                      0x1p-18f * ((fabsf(n.x.y) + fabsf(n.y.y)) + fabsf(n.z.y))};
     const v2 nd = -vfma(n.z, pos.z, vfma(n.y, pos.y, n.x * pos.x));  // -N.P
@@ -462,14 +487,8 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
                 : "=&v"(x1), "=&v"(y1), "=&v"(z1), "=&v"(x0), "=&v"(y0), "=&v"(z0)
                 : "v"(la)
                 : "memory");
-            push_skip_bits(ma, mb, x1.w, y1.w, z1.w, n, kb);
-            push_skip_bits(ma, mb, x1.z, y1.z, z1.z, n, kb);
-            push_skip_bits(ma, mb, x1.y, y1.y, z1.y, n, kb);
-            push_skip_bits(ma, mb, x1.x, y1.x, z1.x, n, kb);
-            push_skip_bits(ma, mb, x0.w, y0.w, z0.w, n, kb);
-            push_skip_bits(ma, mb, x0.z, y0.z, z0.z, n, kb);
-            push_skip_bits(ma, mb, x0.y, y0.y, z0.y, n, kb);
-            push_skip_bits(ma, mb, x0.x, y0.x, z0.x, n, kb);
+            push_skip_bits4(ma, mb, x1, y1, z1, n, kb);
+            push_skip_bits4(ma, mb, x0, y0, z0, n, kb);
         }
     };
     const int n0 = nl < 32 ? nl : 32;
@@ -499,10 +518,21 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
             c1 &= ~ob;
         }
     }
+    // Lights that may come closer than the distance window: the item's window test, per pixel (rare).
+    bool near_a = false, near_b = false;
+    for (uint64_t cm = close_m; cm != 0; cm &= cm - 1) {  // uniform
+        const int j = __builtin_ctzll(cm);
+        const f3x2 l = f3x2{splat(lds_lights[j]) - pos.x, splat(lds_lights[kBalLdsStride + j]) - pos.y,
+                            splat(lds_lights[2 * kBalLdsStride + j]) - pos.z};
+        const m2 ok = ge(sqrt_nr(dot3(l, l)), dist_lo);
+        const uint32_t bit = 1u << (j & 31);
+        near_a = near_a || (((j < 32 ? a0 : a1) & bit) != 0 && !on(ok.x));
+        near_b = near_b || (((j < 32 ? c0 : c1) & bit) != 0 && !on(ok.y));
+    }
 
     BAL_PROF_T(t1);
     BAL_PROF_ADD(0, t1 - t0);
-    return BalMasks{a0, a1, c0, c1};
+    return BalMasks{a0, a1, c0, c1, near_a, near_b};
 }
 
 // The wave's live (pixel, light) items -- the popcounts of its pixels' live masks, summed over the wave: the
@@ -513,6 +543,7 @@ __device__ __forceinline__ int wave_live_items(const BalMasks& bm) {
     for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
     return __builtin_amdgcn_readfirstlane(c);
 }
+
 
 // The whole balanced pass over the point lights of an untiled lean wave (at most kBalMaxLights). `live_a` /
 // `live_b` say which of the pair's pixels take part (geometry); `lds_lights`: the pass's point lights staged by
@@ -529,6 +560,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
                                                          m2& redo, unsigned long long* bal_prof = nullptr) {
     const int lane_id = (int)(threadIdx.x & 63);
     const uint32_t a0 = bm.a0, a1 = bm.a1, c0 = bm.c0, c1 = bm.c1;
+    redo |= mask2(bm.near_a, bm.near_b);  // pass 1's distance window (the items carry no test)
     constexpr int R = EXACT ? kBalRecX : kBalRec;  // record stride (float4)
     BAL_PROF_T(t1);
 

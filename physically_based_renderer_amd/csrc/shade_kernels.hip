@@ -943,7 +943,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 // q2 above is not used on this path, so it is not live across pass 1); after the loop the
                 // unscaled ones once more for the finish. launder() keeps the compiler from merging the
                 // rebuilds with the computation above (which would keep q2 live across the loop: it spilled).
-                const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, s.bal[wave_id], s.bal_light, prof);
+                const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoFaithful, s.bal[wave_id],
+                                                   s.bal_light, prof);
                 bal_items = wave_live_items(bm);
                 launder(p);
                 q2 = pair_invariants(p, ps, fast2);
@@ -1005,7 +1006,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                     p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? rrow : 0, vb ? rrow + 1 : 0,
                                                       vb && gb.pairs_aligned);
                 };
-                const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, s.bal[wave_id], s.bal_light, prof);
+                const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoExact, s.bal[wave_id],
+                                                   s.bal_light, prof);
                 bal_items = wave_live_items(bm);
                 q2 = pair_invariants(p, ps, fast2);
                 d2 = lighting_fast<false, true, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
@@ -1632,10 +1634,10 @@ hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels,
 // This unit's build record (pbr_build_info.h, pbr_build_info): the stamp, flavor and flags it was compiled with and
 // every build switch of the kernels as the preprocessor saw it.
 #include "pbr_build_info.h"
-#define PBR_KERNEL_SWITCHES                                                                                        \
-    PBR_BI_SWITCH(PBR_X2_MIN_WAVES) ", " PBR_BI_SWITCH(PBR_LEAN_MIN_WAVES) ", " PBR_BI_SWITCH(PBR_LEAN_UNIFORM_MIN_WAVES) \
-    ", " PBR_BI_SWITCH(PBR_BAL_PROFILE) ", " \
-    PBR_BI_SWITCH(PBR_WAVE_TIMELINE) ", " PBR_BI_SWITCH(PBR_DEBUG_BOUNDS) ", " PBR_BI_SWITCH(PBR_SPLIT_BAL) ", "   \
+#define PBR_KERNEL_SWITCHES                                                                                   \
+    PBR_BI_SWITCH(PBR_X2_MIN_WAVES) ", " PBR_BI_SWITCH(PBR_LEAN_MIN_WAVES) ", "                                 \
+    PBR_BI_SWITCH(PBR_LEAN_UNIFORM_MIN_WAVES) ", " PBR_BI_SWITCH(PBR_BAL_PROFILE) ", "                          \
+    PBR_BI_SWITCH(PBR_WAVE_TIMELINE) ", " PBR_BI_SWITCH(PBR_DEBUG_BOUNDS) ", " PBR_BI_SWITCH(PBR_SPLIT_BAL) ", " \
     PBR_BI_SWITCH(PBR_POW5_LDS) ", " PBR_BI_SWITCH(PBR_POW5_GLIBC_FROM) ", "                                     \
     PBR_BI_SWITCH(PBR_POW5_FAST3_GLIBC_FROM) ", " PBR_BI_SWITCH(PBR_FAITHFUL_GAMMA_LO) ", "                      \
     PBR_BI_SWITCH(PBR_ATAN2F_KMAX)

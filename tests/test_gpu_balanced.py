@@ -319,3 +319,65 @@ def test_default_balancing_minimum(mode, n_lights, ctx_default, ctx_pair, gpu):
     expect = want_bal if n_lights >= minimum else want_plain
     assert O.bit_equal(got, expect).all()
     check_mode(mode, got, want_plain, ref)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_balanced_distance_window_in_pass1(mode, ctx_pair, gpu):
+    """The items' distance window (faithful dist >= 0.01, exact >= 2^-20: point_or_spot_*_x2) as pass 1 decides it
+    (balanced_pass1: a light whose nearest box point is >= 1.02 x the window from the wave's box needs no test; for
+    another one each pixel with the light live runs the item's own test, and a failing pixel is redone on the exact
+    path). Row 0: pixels facing light 0 at distances straddling 0.01 and 2^-20 (and on it); row 1: the same distances
+    behind the pixels (N.L < 0: the items are skipped, no redo is needed); rows 2-3: ordinary pixels of the same
+    waves, farther away. Exact: bit-identical to the uniform loop and the oracle; faithful: 1e-5 of the oracle."""
+    rng = np.random.default_rng(31)
+    w, h, nl = 128, 4, 24
+    planes, lights = _scene(rng, w, h, nl)
+    lights[0, 8:11] = (1.0, 2.0, 3.0)
+    dists = np.array([0.0, 2.0 ** -21, 2.0 ** -20, 1.5 * 2.0 ** -20, 1e-3, 0.0099, 0.00999999, 0.01, 0.01000001,
+                      0.0101, 0.0102, 0.0103, 0.011, 0.02, 0.05, 0.5], np.float32)
+    for r, side in ((0, 1.0), (1, -1.0)):
+        planes[0:3, r, :16] = np.array([1.0, 2.0, 3.0], np.float32)[:, None]
+        planes[2, r, :16] = np.float32(3.0) - dists  # light 0 at +dist along z from the pixel
+        planes[3:6, r, :16] = np.array([0.0, 0.0, side], np.float32)[:, None]
+    flags = N.PBR_FLAG_FAITHFUL if mode == "faithful" else 0
+    pc = PassConstants(num_point_lights=nl, lights_array=lights, flags=flags)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc)
+    want, redo_p = run(plain, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    print(f"distance window ({mode}): redo {redo_b} vs {redo_p}")
+    assert 0 < redo_b <= redo_p  # the pixels facing light 0 within the window are redone
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    check_mode(mode, got, want, ref)
+
+
+@pytest.mark.parametrize("heavy", [0.78, 0.5, 0.95])
+def test_balanced_faithful_uneven_waves(heavy, ctx_pair, gpu):
+    """Waves whose pixels' live counts are far from even (the case the ranking pairs up): `heavy` of the pixels (more
+    on later rows) face all 64 lights, the rest face none, and a fifth take random normals. Within 1e-5 of the oracle
+    and within the association bound of the unbalanced kernel."""
+    rng = np.random.default_rng(int(heavy * 1000))
+    w, h, nl = 256, 8, 64
+    planes, lights = _scene(rng, w, h, nl)
+    lights[:, 8:11] = np.stack([rng.uniform(-20, 20, nl), rng.uniform(-20, 20, nl), rng.uniform(-30, -15, nl)], 1)
+    planes[2] = rng.uniform(0, 5, (h, w))
+    face = rng.uniform(0, 1, (h, w)) < heavy * (0.6 + 0.1 * np.arange(h))[:, None]
+    randn = rng.uniform(0, 1, (h, w)) < 0.2
+    planes[3:6] = np.where(face, np.array([0.0, 0.0, -1.0], np.float32)[:, None, None],
+                           np.array([0.0, 0.0, 1.0], np.float32)[:, None, None])
+    rn = rng.normal(size=(3, h, w)).astype(np.float32)
+    rn /= np.linalg.norm(rn, axis=0, keepdims=True)
+    planes[3:6] = np.where(randn, rn, planes[3:6])
+    pc = PassConstants(num_point_lights=nl, lights_array=lights, flags=N.PBR_FLAG_FAITHFUL)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc)
+    st = bal.pass_stats()
+    want, redo_p = run(plain, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    e = O.rel_err(got, ref)
+    print(f"uneven waves (heavy {heavy}): max_rel {e.max():.3g}, light terms {st['light_terms']}, redo {redo_b}")
+    assert redo_b <= redo_p
+    assert close(got, want)
+    assert e.max() <= REL_TOL

@@ -16,9 +16,10 @@ OUT="$ROOT/abx/$NAME"
 mkdir -p "$OBJ" "$OUT"
 HIPCC=/opt/rocm/bin/hipcc
 SHA="$(python3 "$ROOT/physically_based_renderer_amd/_sources.py")"
-FLAVOR="variant: $NAME ${FLAGS//\"/\'}"
+FLAVOR="variant: $NAME ${FLAGS//[\"\']/}"
 COMMON="-O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -I$ROOT/include -I$CSRC -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt --offload-arch=gfx950 -munsafe-fp-atomics"
-prov() { echo "-DPBR_SOURCES_SHA=\"$SHA\" -DPBR_BUILD_FLAVOR=\"$FLAVOR\" -DPBR_UNIT_CFLAGS=\"$1\""; }
+# single-quoted for the eval below, so each define keeps its double quotes (a C string) and its spaces
+prov() { echo "'-DPBR_SOURCES_SHA=\"$SHA\"' '-DPBR_BUILD_FLAVOR=\"$FLAVOR\"' '-DPBR_UNIT_CFLAGS=\"$1\"'"; }
 eval $HIPCC $COMMON $FLAGS $(prov "") -c "$CSRC/shade_kernels_bal.hip" -o "$OBJ/shade_kernels_bal.o"
 if [ "$MODE" = full ]; then
   ILP="-mllvm -amdgpu-sched-strategy=max-ilp"

@@ -83,10 +83,11 @@ def main():
     lines = kernel_lines(ASM, KERNEL)
     bl = blocks_of(lines)
     ri = next(k for k, b in enumerate(bl) if any("offset:1360" in l for l in b[2]))
-    hk = max(k for k in range(ri + 1) if "Inner Loop Header" in bl[k][1])
+    hk = max(k for k in range(ri + 1) if "Loop Header" in bl[k][1])
     hdr = bl[hk][0].lstrip(".")  # e.g. LBB8_612 -> the blocks of its loop carry "Header=BB8_612"
     tag = "Header=" + hdr[1:]
-    loop = [b for k, b in enumerate(bl) if k == hk or tag in b[1]]
+    # (a nested loop -- the faithful pieces' advance -- carries "Parent Loop BB8_612" on its blocks)
+    loop = [b for k, b in enumerate(bl) if k == hk or tag in b[1] or ("Parent Loop " + hdr[1:]) in b[1]]
     # main path: the header and the fall-through blocks that follow it up to the one holding the done-mask compare
     main_blocks, k = [], hk
     while True:
