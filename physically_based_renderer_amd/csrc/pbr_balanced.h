@@ -249,16 +249,8 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ float bal_wave_min(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
-}
-__device__ __forceinline__ float bal_wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-    return v;
-}
+__device__ __forceinline__ float bal_wave_min(float v) { return wave_min_dpp(v); }
+__device__ __forceinline__ float bal_wave_max(float v) { return wave_max_dpp(v); }
 
 // Pass 1 for the pair and four lights j..j+3 (coordinates x, y, z: one float4 per axis, light j + i in element i):
 // shift the lights' SKIP bits for each pixel (the sign of t1, see the header comment) into `ma` / `mb`, light j + 3
@@ -538,10 +530,7 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
 // The wave's live (pixel, light) items -- the popcounts of its pixels' live masks, summed over the wave: the
 // point-light terms pass 2 evaluates (statistics: pbr_pass_stats::light_terms). Wave-uniform result.
 __device__ __forceinline__ int wave_live_items(const BalMasks& bm) {
-    int c = (__popc(bm.a0) + __popc(bm.a1)) + (__popc(bm.c0) + __popc(bm.c1));
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
-    return __builtin_amdgcn_readfirstlane(c);
+    return wave_sum_dpp((__popc(bm.a0) + __popc(bm.a1)) + (__popc(bm.c0) + __popc(bm.c1)));
 }
 
 
@@ -574,12 +563,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     const int pos_b = atomicAdd(&w.hist[bin_b], 1);
     wave_lds_sync();
     const int h = w.hist[lane_id];
-    int incl = h;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int t = __shfl_up(incl, off, 64);
-        if (lane_id >= off) incl += t;
-    }
+    const int incl = wave_scan_add_dpp(h);
     wave_lds_sync();
     w.hist[lane_id] = incl - h;  // exclusive prefix: first rank of each bin
     wave_lds_sync();

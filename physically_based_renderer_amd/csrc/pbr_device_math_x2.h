@@ -32,6 +32,57 @@ __device__ __forceinline__ m2& operator|=(m2& a, m2 b) { return a = a | b; }
 __device__ __forceinline__ m2 mask2(bool x, bool y) { return m2{lanes(x), lanes(y)}; }
 __device__ __forceinline__ m2 all2(bool c) { const uint64_t m = lanes(c); return m2{m, m}; }
 
+// ---- Wave-wide reductions and scans on the DPP network (no LDS round trips) ----
+// __shfl_xor / __shfl_up compile to ds_bpermute: each step an LDS round trip (and its address arithmetic), six in a
+// row per reduction. Here the first four steps are DPP lane moves fused into the combining instruction (quad_perm
+// [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: every lane of a 16-lane row then holds the row's result), and
+// the rows meet on the scalar unit (v_readlane of lanes 0, 16, 32, 48). Min / max run on an integer key whose signed
+// order is the float order (non-NaN floats; -0 below +0, which changes no value computed from the result); a NaN
+// input counts as `neutral` (fminf / fmaxf also ignore a NaN operand). The result is wave-uniform (SGPR).
+template <int CTRL>
+__device__ __forceinline__ int dpp_row_move(int v) {  // sources always inside the row: bound_ctrl lets it fuse
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ int float_key(float f) {
+    const int b = __builtin_bit_cast(int, f);
+    return b ^ (int)((uint32_t)(b >> 31) >> 1);
+}
+__device__ __forceinline__ float key_float(int k) { return __builtin_bit_cast(float, k ^ (int)((uint32_t)(k >> 31) >> 1)); }
+template <bool MAX>
+__device__ __forceinline__ float wave_minmax_dpp(float v, float neutral) {
+    int k = float_key(v == v ? v : neutral);
+    auto op = [](int a, int b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+    k = op(k, dpp_row_move<0xB1>(k));   // quad_perm [1,0,3,2]
+    k = op(k, dpp_row_move<0x4E>(k));   // quad_perm [2,3,0,1]
+    k = op(k, dpp_row_move<0x141>(k));  // row_half_mirror
+    k = op(k, dpp_row_move<0x140>(k));  // row_mirror
+    const int r = op(op(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
+                     op(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
+    return key_float(r);
+}
+__device__ __forceinline__ float wave_min_dpp(float v, float neutral = 3.0e38f) { return wave_minmax_dpp<false>(v, neutral); }
+__device__ __forceinline__ float wave_max_dpp(float v, float neutral = -3.0e38f) { return wave_minmax_dpp<true>(v, neutral); }
+// Sum over the wave, wave-uniform.
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += dpp_row_move<0xB1>(v);
+    v += dpp_row_move<0x4E>(v);
+    v += dpp_row_move<0x141>(v);
+    v += dpp_row_move<0x140>(v);
+    return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
+           (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
+}
+// Inclusive prefix sum over the lanes: row_shr 1, 2, 4, 8 within each row (lanes shifted in from outside it read 0),
+// then row_bcast 15 / 31 carry each row's total into the rows above.
+__device__ __forceinline__ int wave_scan_add_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
 struct f3x2 {
     v2 x, y, z;
 };

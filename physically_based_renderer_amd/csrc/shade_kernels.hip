@@ -103,16 +103,8 @@ struct TileBounds {
     float mn[3], mx[3];
 };
 
-__device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-    return v;
-}
+__device__ __forceinline__ float wave_min(float v) { return wave_min_dpp(v); }  // pbr_device_math_x2.h
+__device__ __forceinline__ float wave_max(float v) { return wave_max_dpp(v); }
 
 struct Lds {
     union {

@@ -6,6 +6,8 @@
 * quarter_dot_probe.hip -- the faithful loop's power-of-two rescaled invariants (faithful_scale): N/4 . H
   is exactly N.H / 4 in the fast window, so the dot's clamp bit gives max(N.H, 0) / 4 in lean waves, the
   GGX denominator keeps the reference's bits, and faithful_unscale restores every invariant;
+* wave_ops_probe.hip -- the DPP wave reductions and scan of pbr_device_math_x2.h (the culling box, pass 1's box and
+  bounds, the balanced ranking's prefix sum) against a serial evaluation;
 * libm_probe.hip -- the device build of libm_f32.h (WorldToSkyUV's atan2f / asinf) returns the host
   glibc's bits: asinf on every float in [-1, 1], atanf on every finite float, and 2^27 random
   atan2f pairs.
@@ -29,7 +31,7 @@ FLAGS = ["-O3", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result", "-fPIC"
 def probes(tmp_path_factory, gpu):
     d = tmp_path_factory.mktemp("probes")
     libs = {}
-    for name in ("fastdiv_probe", "libm_probe", "sqrt_probe", "gamma_probe", "quarter_dot_probe"):
+    for name in ("fastdiv_probe", "libm_probe", "sqrt_probe", "gamma_probe", "quarter_dot_probe", "wave_ops_probe"):
         so = str(d / f"{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, os.path.join(ROOT, "tests", "hip", f"{name}.hip"), "-o", so,
                         "-lpthread"], check=True)
@@ -151,3 +153,33 @@ def test_faithful_quarter_dots_are_exact(probes, lean):
     assert list(bad[:3]) == [0, 0, 0]
     if lean:  # control: the samples reach N.H > 1, where saturating the unscaled dot would have clamped
         assert bad[3] > 0
+
+
+def test_dpp_wave_reductions_and_scan(probes):
+    """wave_min_dpp / wave_max_dpp (integer keys, NaN counted as the neutral value, as fminf / fmaxf ignore it),
+    wave_sum_dpp and the inclusive wave_scan_add_dpp against numpy, on waves of random floats over many binades with
+    +-0, +-inf, NaN and denormals mixed in, one wave all NaN (-> the neutral values), and random ints."""
+    import numpy as np
+
+    rng = np.random.default_rng(2024)
+    n = 4096
+    f = (rng.standard_normal(64 * n) * np.exp2(rng.integers(-60, 60, 64 * n))).astype(np.float32)
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-40, 3.0e38, -3.0e38], np.float32)
+    pick = rng.random(64 * n) < 0.05
+    f[pick] = rng.choice(specials, pick.sum())
+    f[64 * 7:64 * 8] = np.nan
+    iv = rng.integers(-1000, 1000, 64 * n).astype(np.int32)
+    mn, mx = np.empty(n, np.float32), np.empty(n, np.float32)
+    sm, sc = np.empty(n, np.int32), np.empty(64 * n, np.int32)
+    P = ctypes.POINTER
+    fn = probes["wave_ops_probe"].probe_wave_ops
+    assert fn(f.ctypes.data_as(P(ctypes.c_float)), iv.ctypes.data_as(P(ctypes.c_int)), n,
+              mn.ctypes.data_as(P(ctypes.c_float)), mx.ctypes.data_as(P(ctypes.c_float)),
+              sm.ctypes.data_as(P(ctypes.c_int)), sc.ctypes.data_as(P(ctypes.c_int))) == 0
+    w = f.reshape(n, 64)
+    want_mn = np.where(np.isnan(w), np.float32(3.0e38), w).min(axis=1)
+    want_mx = np.where(np.isnan(w), np.float32(-3.0e38), w).max(axis=1)
+    assert np.array_equal(mn, want_mn) and np.array_equal(mx, want_mx)  # -0 == +0 here; the values are the point
+    assert mn[7] == np.float32(3.0e38) and mx[7] == np.float32(-3.0e38)
+    assert np.array_equal(sm, iv.reshape(n, 64).sum(axis=1))
+    assert np.array_equal(sc, np.cumsum(iv.reshape(n, 64), axis=1).reshape(-1))
