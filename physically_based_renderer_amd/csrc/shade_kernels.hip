@@ -1136,7 +1136,8 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         return;
     }
     const int64_t row = (int64_t)y * gb.row_stride;
-    __shared__ v2 s_park[4][64];   // uniform-loop faithful waves: albedo, 1 - metallic across the light loop
+    constexpr bool kPark = lean_min_waves<AMBIENT, CULL, FAITHFUL>() >= 5;
+    __shared__ v2 s_park[4][64];   // five-wave kernels' faithful waves: albedo, 1 - metallic across the light loop
     bool need_a, need_b;           // pixels for the IEEE path (the exact re-pass)
     bool faithful_wave = false;    // wave-uniform
     int kept_total = 0;
@@ -1208,11 +1209,11 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
         f3x2 d2;
         if (faithful_wave) {
             if (!CULL) faithful_scale(q2);
-            // Uniform-loop (5-wave) kernels: albedo and 1 - metallic feed the faithful loop only through make_faithful's
-            // hoisted products, but the finish needs them; parked in LDS across the loop (the memory clobber keeps the
+            // Five-wave kernels: albedo and 1 - metallic feed the faithful loop only through make_faithful's hoisted
+            // products, but the finish needs them; parked in LDS across the loop (the memory clobber keeps the
             // compiler from forwarding the stored values), they hold no VGPRs there: at the 96-VGPR budget of five
             // waves per SIMD the loop then runs without scratch.
-            if constexpr (!CULL) {
+            if constexpr (kPark) {
                 const int l = (int)(threadIdx.x & 63);
                 s_park[0][l] = q2.albedo.x;
                 s_park[1][l] = q2.albedo.y;
@@ -1226,7 +1227,7 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
             else
                 d2 = lighting_fast<CULL, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo, kept_total,
                                                       nullptr, nullptr, false, false, BalMasks{}, nullptr, &first);
-            if constexpr (!CULL) {
+            if constexpr (kPark) {
                 asm volatile("" ::: "memory");
                 const int l = lane_id_fresh();
                 q2.albedo = f3x2{s_park[0][l], s_park[1][l], s_park[2][l]};
