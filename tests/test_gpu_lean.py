@@ -149,3 +149,52 @@ def test_lean_passes_on_two_streams(lean_ctx, mono_ctx, gpu):
     torch.cuda.synchronize()
     for o in outs:
         assert O.bit_equal(o.cpu().numpy(), ref).all()
+
+
+def light_set(pc, kind):
+    """Config 4's light list recombined (48-byte records: strength, spot power, direction, pad, position, pad):
+    '300pt' -- 300 point lights (the culled walk's first 256 tested on the positions lean_wave preloads, the rest
+    by survivor_masks); '2dir_40pt' -- two directional lights ahead of 40 point lights (the preloaded indices
+    offset by n_dir, a partial chunk); '100pt_20spot' -- spot lights after the points (no preloaded survivors)."""
+    pts = pc.light_array()[: pc.num_point_lights]
+    n_dir, n_pt, n_sp = {"300pt": (0, 300, 0), "2dir_40pt": (2, 40, 0), "100pt_20spot": (0, 100, 20)}[kind]
+    pt = np.concatenate([pts, pts[: max(n_pt - len(pts), 0)].copy()])[:n_pt]
+    pt[len(pts):, 8:11] += np.float32(3.0)  # the repeated lights moved off their originals
+    dirs = np.zeros((n_dir, 12), np.float32)
+    dirs[:, 0:3] = (0.6, 0.5, 0.4)
+    dirs[:, 4:7] = np.asarray([(0.57735026, -0.57735026, 0.57735026), (-0.6, -0.8, 0.0)], np.float32)[:n_dir]
+    spots = pts[:n_sp].copy()
+    spots[:, 3] = 8.0  # spot power
+    spots[:, 4:7] = (0.0, -1.0, 0.0)
+    spots[:, 8:11] += np.float32(1.5)
+    arr = np.concatenate([dirs, pt, spots]).astype(np.float32)
+    return PassConstants(**{**pc.__dict__, "num_dir_lights": n_dir, "num_point_lights": n_pt,
+                            "num_spot_lights": n_sp, "lights": [], "lights_array": arr})
+
+
+@pytest.mark.parametrize("kind", ["300pt", "2dir_40pt", "100pt_20spot"])
+@pytest.mark.parametrize("faithful", [True, False])
+def test_lean_culled_light_sets(kind, faithful, lean_ctx, mono_ctx, gpu):
+    """The culled lean kernel's survivor masks (preloaded for the first 256 point lights when the pass has no spot
+    lights) on light sets config 4 does not have: frames and statistics identical to the monolithic kernel's, and
+    within the bar of the oracle (exact mode bit-identical but for the x^5 residue)."""
+    cfg = S.CONFIGS[4].with_size(517, 45)
+    planes, _ = S.fill_gbuffer_host(cfg)
+    pc = light_set(S.scene_pass(cfg), kind)
+    if faithful:
+        pc = with_flags(pc, N.PBR_FLAG_FAITHFUL)
+    gb = GBuffer.from_host(planes, gpu)
+    a, sa = run(lean_ctx, gb, pc, None)
+    assert "shade_lean_kernel" in lean_ctx.last_kernel()
+    b, sb = run(mono_ctx, gb, pc, None)
+    assert sa["cull_tiles"] > 0 and sa["cull_tile_lights"] > 0  # the pass culled
+    assert O.bit_equal(a, b).all()
+    assert sa == sb
+    ref = O.shade(list(np.ascontiguousarray(planes)), oracle_pass_from_constants(pc), pc.light_array(), None,
+                  n_threads=16)
+    e = O.rel_err(a, ref)
+    print(f"{kind} faithful={faithful}: stats {sa} max_rel={np.nanmax(e):.3g} "
+          f"bit-identical {O.bit_equal(a, ref).mean():.6f}")
+    assert np.nanmax(e) <= REL_TOL
+    if not faithful:
+        assert O.bit_equal(a, ref).mean() >= 0.9999
