@@ -346,7 +346,8 @@ __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const 
 // and two lights, element for element the same operations (the pixel's invariants splat into both elements), so
 // each element's term carries the bits of the uniform loop's term for that (pixel, light), less the range factor,
 // which is exactly 1 for every item pass 1 keeps (faithful_point_items2): the bits are unchanged.
-__device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3x2& lp, const f3x2& ls, m2& ok) {
+__device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3x2& lp, const f3x2& ls, m2& ok,
+                                                   uint64_t live) {
     PixelInvariants2 q;
     q.n = splat3(p.n.x, p.n.y, p.n.z);
     q.v = splat3(p.v.x, p.v.y, p.v.z);
@@ -368,7 +369,7 @@ __device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3
     const f3x2 h = normalize_x2(add3(q.v, l), ok);
     const v2 dsat = max_dsat(dist);
     const v2 att = recip_nr(dsat * dsat).r;
-    return brdf_x2<true>(q, f3x2{ls.x * att, ls.y * att, ls.z * att}, l, h, ok);
+    return brdf_x2<true>(q, f3x2{ls.x * att, ls.y * att, ls.z * att}, l, h, ok, live);
 }
 
 // The live-light masks of the pair's pixels (pass 1), light j at bit j % 32 of word j / 32.
@@ -651,7 +652,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
             f3x2 lp, ls;
             read_pair_lights(lds_lights, j0, j1, lp, ls);
             if constexpr (EXACT) {
-                const f3x2 c = exact_point_items2(cur, lp, ls, oki);
+                const f3x2 c = exact_point_items2(cur, lp, ls, oki, live);
                 accx = mk3((accx.x + c.x.x) + c.x.y, (accx.y + c.y.x) + c.y.y, (accx.z + c.z.x) + c.z.y);
             } else {
                 faithful_point_items2(cur, lp, ls, oki, acc, live);

@@ -133,7 +133,20 @@ __device__ __forceinline__ v2 sqrt_nr(v2 x) {  // see sqrt_nr in pbr_device_math
     const v2 r = vfma(-s0, s0, x);
     return vfma(r, 0.5f * y, s0);
 }
-__device__ __forceinline__ v2 pow5_light(v2 x) { return v2{pow5_light(x.x), pow5_light(x.y)}; }
+// pow5_light for the pair, element for element the same values: the fp64 products of both elements unconditionally
+// (straight-line: the compiler interleaves the two chains with the work around them, where a per-element branch kept
+// each chain in its own block), glibc's algorithm patched in above PBR_POW5_GLIBC_FROM under a wave-uniform branch
+// taken only when a lane of `live` (the lanes whose result is used) needs it.
+__device__ __forceinline__ v2 pow5_light(v2 x, uint64_t live = ~0ull) {
+    const double dx = (double)x.x, dy = (double)x.y;
+    const double dx2 = dx * dx, dy2 = dy * dy;
+    v2 p = v2{(float)(dx2 * dx2 * dx), (float)(dy2 * dy2 * dy)};
+    if (__builtin_expect((lanes(x.x > PBR_POW5_GLIBC_FROM || x.y > PBR_POW5_GLIBC_FROM) & live) != 0, 0)) {
+        if (x.x > PBR_POW5_GLIBC_FROM && on(live)) p.x = pow5_glibc(x.x);
+        if (x.y > PBR_POW5_GLIBC_FROM && on(live)) p.y = pow5_glibc(x.y);
+    }
+    return p;
+}
 // |x| in [lo, hi] per element (false for NaN).
 __device__ __forceinline__ m2 in_win(v2 x, float lo, float hi) {
     v2 a = __builtin_elementwise_abs(x);
@@ -222,7 +235,8 @@ __device__ __forceinline__ v2 div_pi(v2 x) { return vfma(x, splat(kInvPiHi), x *
 //    ndf_g F stays inside the division window for any p: the p == 0 / p >= 2^-40 test is moot.
 //
 template <bool LEAN>
-__device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, m2& ok) {
+__device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, m2& ok,
+                                        uint64_t live = ~0ull) {
     v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
     v2 n_dot_h_sqr = n_dot_h * n_dot_h;
     v2 den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
@@ -233,7 +247,7 @@ __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance
     v2 ggx_l = div_nr(n_dot_l, recip_nr(n_dot_l * q.one_minus_k + q.k));
     v2 g = ggx_l * q.ggx_v;
     v2 cos_theta = dot3_sat(h, q.v);
-    v2 p = pow5_light(1.0f - cos_theta);
+    v2 p = pow5_light(1.0f - cos_theta, live);
     f3x2 f = f3x2{q.f0.x + q.one_minus_f0.x * p, q.f0.y + q.one_minus_f0.y * p, q.f0.z + q.one_minus_f0.z * p};
     v2 ndf_g = ndf * g;
     v2 denom = q.four_n_dot_v * n_dot_l + 0.001f;
