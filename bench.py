@@ -52,6 +52,10 @@ EXIT_PROVENANCE = 4  # ... when the loaded library is not the product build of t
 # Environment variables that only route the transport of the multi-rank run; every other PBR_* variable changes which
 # library or kernel runs (PBR_LIB_PATH, PBR_BALANCED_MIN, PBR_LEAN, PBR_PIXELS_PER_THREAD, ...): a development setting.
 ENV_NEUTRAL = ("PBR_DIST_TIMEOUT_S", "PBR_DIST_INIT_METHOD")
+# Version of the line's keys, bumped when a key changes meaning (6: hbm_gbps = the kernel's own bytes, hbm_gbps_model
+# = SURVEY 8(d)'s; pcie_h2d_gbps = the warm link rate, pcie_h2d_first_gbps = the first copy; roofline.bound_unit,
+# frac_profile, launch_vs_profile). Lines without the key are rounds 1-5.
+LINE_SCHEMA = 6
 
 
 def log(*a):
@@ -149,6 +153,11 @@ def load_pmc(workload: str, head: str, path: str = os.path.join(ROOT, "profiles"
         return None, None, {"profile": None, "kernel_sources_sha": head}
     prov = {"profile": e.get("source"), "profile_kernel_sources_sha": e.get("kernel_sources_sha"),
             "kernel_sources_sha": head, "profile_revision": e.get("kernel_revision")}
+    # The profiled box's own kernel time (rocprofv3 kernel trace, mean over the profiled run's timed launches): counter
+    # ratios transfer between boxes, durations do not, so the line shows which box its traffic figure came from.
+    kt = e.get("kernel_trace") or {}
+    if kt.get("mean_ms_timed_steps") is not None:
+        prov["profile_kernel_mean_ms"] = round(float(kt["mean_ms_timed_steps"]), 4)
     if e.get("kernel_sources_sha") != head:
         prov["stale"] = True
         return None, None, prov
@@ -157,6 +166,66 @@ def load_pmc(workload: str, head: str, path: str = os.path.join(ROOT, "profiles"
         return float(e["hbm_bytes_per_launch"]), (None if busy is None else round(float(busy), 3)), prov
     except (KeyError, TypeError, ValueError):
         return None, None, prov
+
+
+def roofline_block(fpp, fpp_exec, bpp, bpp_read, px, avg_kernel_s, median_kernel_ms, traffic, valu_busy, pmc_prov,
+                   kernel_name, stats) -> dict:
+    """The line's `roofline` object for the dominant kernel (one launch = one pass over `px` pixels).
+
+    At 64 lights the arithmetic intensity (fpp / bpp ~ 93 FLOP/B) is 5x the ridge point, so the FP32 vector (VALU) roof
+    bounds the kernel: 157.3 TF (MI355X_MICROARCH.md). There is no matrix op on this path: `bound` keeps the
+    contract's vocabulary ("mfma" = the compute roof, "hbm") and `bound_unit` names the unit that roof really is
+    ("valu" or "hbm"). `frac` comes from this run's HIP events; `frac_profile` from the committed profile's kernel-trace
+    mean (pmc.profile_kernel_mean_ms, the box the traffic counters came from), and `launch_vs_profile` is this run's
+    mean launch over that one: boxes of this pool differ by up to ~5% for one build."""
+    compute_bound = fpp / bpp > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
+    achieved = bpp * px / avg_kernel_s / 1e9
+    hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBPS, 5),
+           "bytes_per_px": bpp, "bytes_per_px_read": bpp_read,
+           "achieved_read": round(bpp_read * px / avg_kernel_s / 1e9, 2)}
+    tflops = fpp * px / avg_kernel_s / 1e12
+    tflops_exec = fpp_exec * px / avg_kernel_s / 1e12
+    prof_ms = (pmc_prov or {}).get("profile_kernel_mean_ms")
+    quoted = prof_ms is not None and not (pmc_prov or {}).get("stale")
+    frac_profile = None
+    if quoted:
+        frac_profile = (round(fpp * px / (prof_ms / 1e3) / 1e12 / FP32_PEAK_TFLOPS, 4) if compute_bound else
+                        round(bpp * px / (prof_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 5))
+    return {
+        "bound": "mfma" if compute_bound else "hbm",
+        "bound_unit": "valu" if compute_bound else "hbm",
+        "achieved": round(tflops, 3) if compute_bound else hbm["achieved"],
+        "peak": FP32_PEAK_TFLOPS if compute_bound else HBM_PEAK_GBPS,
+        "unit": "TFLOP/s" if compute_bound else "GB/s",
+        "frac": round(tflops / FP32_PEAK_TFLOPS, 4) if compute_bound else hbm["frac"],
+        "frac_profile": frac_profile,
+        "launch_vs_profile": round(avg_kernel_s * 1e3 / prof_ms, 4) if quoted else None,
+        "traffic": traffic,
+        "compute_unit": "valu (fp32 vector ALU; no MFMA on this path)" if compute_bound else None,
+        "kernel": kernel_name, "avg_launch_ms": round(avg_kernel_s * 1e3, 4),
+        "median_launch_ms": round(median_kernel_ms, 4),
+        "flop_per_px": fpp, "bytes_per_px": bpp, "bytes_per_px_read": bpp_read, "px_per_launch": px,
+        "executed_flop_per_px": fpp_exec,
+        "achieved_executed": round(tflops_exec, 3),
+        "frac_executed": round(tflops_exec / FP32_PEAK_TFLOPS, 4),
+        "pass_stats": {k: stats[k] for k in ("geometry_pixels", "light_terms", "backface_tests",
+                                             "cull_tiles", "exact_pixels")},
+        "hbm": hbm,
+        "valu_issue_busy": valu_busy,
+        "pmc": pmc_prov,
+        "note": ("bound: the contract's vocabulary ('mfma' = the compute roof); bound_unit: the unit that roof is -- "
+                 "the FP32 vector ALU (VALU, 157.3 TF packed; no matrix op on this path); frac / achieved count SURVEY "
+                 "8(d)'s algorithmic-model FLOPs (every light for every pixel, which the kernel does not all evaluate) "
+                 "over this run's HIP-event launch mean; frac_profile the same over the committed profile's kernel-trace "
+                 "mean (pmc.profile_kernel_mean_ms; launch_vs_profile = this box / the profiled box); frac_executed / "
+                 "achieved_executed are the utilisation figure: only the terms the kernel evaluated (pass_stats: "
+                 "back-facing terms skipped by the wave-balanced lists and culled lights are not credited; the "
+                 "lists' back-face tests are); kernel = pbr_last_pass_kernel; traffic = rocprofv3 "
+                 "FETCH_SIZE x2 + WRITE_SIZE bytes per launch and valu_issue_busy = SQ_ACTIVE_INST_VALU over "
+                 "kernel cycles, from profiles/pmc_summary.json, quoted only when its kernel_sources_sha "
+                 "equals this build's (pmc)"),
+    }
 
 
 def host_cpu_budget() -> dict:
@@ -631,7 +700,8 @@ def main():
         band_px = cfg.width * band.rows
         bpp = bytes_per_pixel(pc, 4 if rgba8 else 16)
         bpp_read = bytes_read_per_pixel(pc, 4 if rgba8 else 16)
-        achieved = bpp * band_px / avg_kernel_s / 1e9
+        achieved_read = bpp_read * band_px / avg_kernel_s / 1e9  # the bytes the kernel moves (hbm_gbps)
+        achieved_model = bpp * band_px / avg_kernel_s / 1e9  # SURVEY 8(d)'s model (roofline.hbm.achieved)
         traffic, valu_busy, pmc_prov = load_pmc(workload + ("_ao" if pc.flags & N.PBR_FLAG_APPLY_AO else "")
                                                 + ("_rgba8" if rgba8 and not banded else "")
                                                 + ("_faithful" if args.mode == "faithful" else ""),
@@ -639,46 +709,8 @@ def main():
         tile_px = 256 if os.environ.get("PBR_PIXELS_PER_THREAD") == "1" else 128  # culling unit: 32x8 / 64x2
         fpp = flops_per_pixel(pc, cull_note.get("lights_per_tile"), tile_px)
         fpp_exec = executed_flops_per_pixel(pc, stats, band_px)
-        tflops = fpp * band_px / avg_kernel_s / 1e12
-        tflops_exec = fpp_exec * band_px / avg_kernel_s / 1e12
-        # At 64 lights the arithmetic intensity (fpp / bpp ~ 99 FLOP/B) is 5x the ridge point, so the
-        # FP32 vector (VALU) roof bounds the kernel: 157.3 TF (MI355X_MICROARCH.md). There is no matrix op
-        # on this path; "mfma" is the contract's name for the compute roof, and "compute_unit" says which unit
-        # that roof is: the VALU. HBM is reported beside it.
-        compute_bound = fpp / bpp > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBPS * 1e9)
-        hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-               "frac": round(achieved / HBM_PEAK_GBPS, 5),
-               "bytes_per_px": bpp, "bytes_per_px_read": bpp_read,
-               "achieved_read": round(bpp_read * band_px / avg_kernel_s / 1e9, 2)}
-        roofline = {
-            "bound": "mfma" if compute_bound else "hbm",
-            "achieved": round(tflops, 3) if compute_bound else hbm["achieved"],
-            "peak": FP32_PEAK_TFLOPS if compute_bound else HBM_PEAK_GBPS,
-            "unit": "TFLOP/s" if compute_bound else "GB/s",
-            "frac": round(tflops / FP32_PEAK_TFLOPS, 4) if compute_bound else hbm["frac"],
-            "traffic": traffic,
-            "compute_unit": "valu (fp32 vector ALU; no MFMA on this path)" if compute_bound else None,
-            "kernel": kernel_name, "avg_launch_ms": round(avg_kernel_s * 1e3, 4),
-            "median_launch_ms": round(median_kernel_ms, 4),
-            "flop_per_px": fpp, "bytes_per_px": bpp, "bytes_per_px_read": bpp_read, "px_per_launch": band_px,
-            "executed_flop_per_px": fpp_exec,
-            "achieved_executed": round(tflops_exec, 3),
-            "frac_executed": round(tflops_exec / FP32_PEAK_TFLOPS, 4),
-            "pass_stats": {k: stats[k] for k in ("geometry_pixels", "light_terms", "backface_tests",
-                                                 "cull_tiles", "exact_pixels")},
-            "hbm": hbm,
-            "valu_issue_busy": valu_busy,
-            "pmc": pmc_prov,
-            "note": ("compute roof = the FP32 vector ALU (VALU, 157.3 TF packed; no matrix op on this path; 'mfma' is "
-                     "the contract's name for the compute roof); frac / achieved count SURVEY 8(d)'s algorithmic-model "
-                     "FLOPs (every light for every pixel, which the kernel does not all evaluate); frac_executed / "
-                     "achieved_executed are the utilisation figure: only the terms the kernel evaluated (pass_stats: "
-                     "back-facing terms skipped by the wave-balanced lists and culled lights are not credited; the "
-                     "lists' back-face tests are); kernel = pbr_last_pass_kernel; traffic = rocprofv3 "
-                     "FETCH_SIZE x2 + WRITE_SIZE bytes per launch and valu_issue_busy = SQ_ACTIVE_INST_VALU over "
-                     "kernel cycles, from profiles/pmc_summary.json, quoted only when its kernel_sources_sha "
-                     "equals this build's (pmc)"),
-        }
+        roofline = roofline_block(fpp, fpp_exec, bpp, bpp_read, band_px, avg_kernel_s, median_kernel_ms, traffic,
+                                  valu_busy, pmc_prov, kernel_name, stats)
         cpu = None
         parity = {}
         exact_leg = None
@@ -728,16 +760,21 @@ def main():
                        "tiled_culling": bool(pc.flags & N.PBR_FLAG_TILED_CULLING),
                        "apply_ao": bool(pc.flags & N.PBR_FLAG_APPLY_AO),
                        "parallelism": f"row-bands x{world}"},
-            "hbm_gbps": round(achieved, 2),
+            # HBM GB/s of the headline metric: the bytes the kernel itself reads and writes per launch (the 11 planes
+            # it reads + the RGBA write) over the HIP-event launch mean; hbm_gbps_model counts SURVEY 8(d)'s 12-plane
+            # model (with the AO plane the default pass never reads) -- the roofline.hbm figure
+            "hbm_gbps": round(achieved_read, 2),
+            "hbm_gbps_model": round(achieved_model, 2),
             "roofline": roofline,
             "cpu_baseline": cpu,
             **parity, **gather_note, **cull_note, **scale,
             **({"exact_mode": exact_leg} if exact_leg is not None else {}),
-            # pinned staging -> HBM: the first copy of the process (allocation + first DMA use of the pinned
-            # pages; the key's meaning in rounds 1-3 and again from round 5) and the same copy repeated into the
-            # resident buffer (the link rate); DESIGN.md §6
-            "pcie_h2d_gbps": round(staging.numel() * 4 / t_upload[0] / 1e9, 2),
-            "pcie_h2d_warm_gbps": round(staging.numel() * 4 / t_upload[1] / 1e9, 2),
+            # pinned staging -> HBM: pcie_h2d_gbps = the copy repeated into the resident buffer (the
+            # link rate; this key's meaning in round 4 and from round 6); pcie_h2d_first_gbps = the process's first
+            # copy (device allocation + first DMA use of the pinned pages). Line schema 6 (line_schema).
+            "pcie_h2d_gbps": round(staging.numel() * 4 / t_upload[1] / 1e9, 2),
+            "pcie_h2d_first_gbps": round(staging.numel() * 4 / t_upload[0] / 1e9, 2),
+            "line_schema": LINE_SCHEMA,
         }
         rc = emit_line(out)
     else:

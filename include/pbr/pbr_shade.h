@@ -21,7 +21,14 @@
  *     order of pbr_set_pass and pbr_shade_* calls decides which pass a shade uses. Contexts expect a
  *     small, long-lived set of streams: the first call on a new stream synchronises the device once,
  *     and past 16 streams the context forgets all but its last one then. Let a stream's passes
- *     finish before destroying it (a new stream may reuse its handle value).
+ *     finish before destroying it (a new stream may reuse its handle value). A light slot or
+ *     texture that grows (more lights than the slot held, a larger map) is released and
+ *     reallocated in stream order on the calling stream (hipFreeAsync / hipMallocAsync after
+ *     stream-side waits for its readers): no device synchronisation. pbr_set_env_map and
+ *     pbr_set_sky_map synchronise their own stream (the host texels may be released on return),
+ *     and pbr_set_pass may wait on the host for the upload that last used its staging slot: call
+ *     them outside a graph capture. pbr_shade_* on a stream the context already knows queues only
+ *     stream-ordered work (event records and waits, the kernel).
  * Plain C types only (hipStream_t is passed as void*).
  */
 #ifndef PBR_SHADE_H

@@ -638,7 +638,10 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     int iters = 0;
 #endif
     {
-        uint64_t live = ~zero;
+        // Lanes outside EXEC are never live: a ballot reports 0 for them, so ~zero alone would keep them live forever
+        // under a partial EXEC (today's callers run this with the full wave; the mask costs one scalar op).
+        const uint64_t exec = __builtin_amdgcn_read_exec();
+        uint64_t live = ~zero & exec;
         while (live != 0) {
 #if PBR_BAL_PROFILE
             ++iters;
@@ -676,7 +679,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
                     if (empty != 0 && on(empty)) put_result();
                 }
             }
-            live = ~zero;
+            live = ~zero & exec;
         }
     }
     BAL_PROF_T(t3);

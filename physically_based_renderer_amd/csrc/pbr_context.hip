@@ -217,18 +217,19 @@ hipError_t before_write(pbr_context* ctx, Resource& r, hipStream_t w, int wi) {
     return hipSuccess;
 }
 
-// Wait on the host for every reader and the writer of `r` (before freeing its memory). Growing a resource is rare, so
-// this synchronises the device: every queued pass that may read `r`, on whatever stream, and its upload are then
-// complete, and no other resource has a pending reader either. It never touches the readers' stream handles, which
-// the caller may have destroyed after their passes finished (or a new stream may have reused): synchronising such a
-// handle failed or waited on an unrelated stream. (A per-pass event of the reader would not do: a context used from
-// one stream records none.)
-hipError_t before_free(pbr_context* ctx, Resource& r) {
-    if (r.readers.empty() && r.writer < 0) return hipSuccess;
-    const hipError_t e = hipDeviceSynchronize();
-    if (e != hipSuccess) return e;
-    forget_readers(ctx);
-    return hipSuccess;
+// Release the memory `p` of resource `r`, which is growing, in stream order on `w` (index wi): `w` waits (stream-side)
+// for the last pass of every other stream that read `r` and for a write of `r` queued on another stream, then the
+// memory goes back to the device's pool with hipFreeAsync. Nothing blocks the host or an unrelated stream, and the
+// sequence is legal inside a graph capture of `w`. A context used from one stream has every reader on `w` itself (a
+// second stream's first launch synchronises the device and clears the records, stream_index), so stream order alone
+// covers them; a multi-stream context records each stream's `last_pass` after every launch. Those events outlive the
+// caller's stream handles, so a reader stream destroyed after its passes finished (the contract, pbr_shade.h) is never
+// touched. The resources are allocated with hipMallocAsync on the writing stream for the same reason.
+hipError_t free_after_readers(pbr_context* ctx, Resource& r, void* p, hipStream_t w, int wi) {
+    hipError_t e = before_write(ctx, r, w, wi);
+    if (e == hipSuccess && r.writer >= 0 && r.writer != wi) e = hipStreamWaitEvent(w, r.written, 0);
+    if (e == hipSuccess && p) e = hipFreeAsync(p, w);
+    return e;
 }
 
 // Record the write of `r` on stream `w` (index wi).
@@ -339,21 +340,24 @@ int pbr_context_destroy(pbr_context* ctx) {
     {
         DeviceGuard g(ctx->device);
         (void)hipDeviceSynchronize();
+        // Light slots and textures come from the stream-ordered pool (hipMallocAsync): returned the same way, after
+        // the synchronisation above, and the pool's frees completed by the one below.
         for (pbr_context::LightSlot& sl : ctx->slots) {
             if (sl.copied) (void)hipEventDestroy(sl.copied);
             if (sl.h) (void)hipHostFree(sl.h);
-            if (sl.d) (void)hipFree(sl.d);
+            if (sl.d) (void)hipFreeAsync(sl.d, nullptr);
             if (sl.use.written) (void)hipEventDestroy(sl.use.written);
         }
         for (pbr_context::Texture* t : {&ctx->env, &ctx->sky}) {
-            if (t->d_u16) (void)hipFree(t->d_u16);
-            if (t->d) (void)hipFree(t->d);
+            if (t->d_u16) (void)hipFreeAsync(t->d_u16, nullptr);
+            if (t->d) (void)hipFreeAsync(t->d, nullptr);
             if (t->use.written) (void)hipEventDestroy(t->use.written);
         }
         for (StreamState& st : ctx->streams) {
             if (st.last_pass) (void)hipEventDestroy(st.last_pass);
             if (st.d_stats) (void)hipFree(st.d_stats);
         }
+        (void)hipDeviceSynchronize();
     }
     delete ctx;
     return PBR_OK;
@@ -389,17 +393,16 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
         sl.copy_pending = false;
     }
     if (n > sl.capacity) {
-        // Growing: the old buffer may still be read by queued passes.
+        // Growing: the old buffer may still be read by queued passes (released after them, in stream order).
         if (sl.d) {
-            e = before_free(ctx, sl.use);
-            if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass slot wait");
-            (void)hipFree(sl.d);
+            e = free_after_readers(ctx, sl.use, sl.d, s, si);
+            if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass slot release");
             sl.d = nullptr;
             sl.capacity = 0;
         }
         int cap = 64;
         while (cap < n) cap *= 2;
-        e = hipMalloc(&sl.d, sizeof(pbr_light) * (size_t)cap);
+        e = hipMallocAsync(reinterpret_cast<void**>(&sl.d), sizeof(pbr_light) * (size_t)cap, s);
         if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass hipMalloc");
         sl.capacity = cap;
     }
@@ -490,16 +493,15 @@ int set_texture(pbr_context* ctx, pbr_context::Texture& t, const void* texels, b
     const int si = stream_index(ctx, s, e);
     if (si < 0) return fail_hip(ctx, e, what);
     if (n > t.capacity) {
-        // Growing: the old texture may still be read by queued passes.
-        e = before_free(ctx, t.use);
+        // Growing: the old texture may still be read by queued passes (released after them, in stream order).
+        e = free_after_readers(ctx, t.use, t.d_u16, s, si);
+        if (e == hipSuccess && t.d) e = hipFreeAsync(t.d, s);
         if (e != hipSuccess) return fail_hip(ctx, e, what);
-        if (t.d_u16) (void)hipFree(t.d_u16);
-        if (t.d) (void)hipFree(t.d);
         t.d_u16 = nullptr;
         t.d = nullptr;
         t.capacity = 0;
-        e = hipMalloc(&t.d_u16, sizeof(uint16_t) * 4 * (size_t)n);
-        if (e == hipSuccess) e = hipMalloc(&t.d, sizeof(float4) * (size_t)n);
+        e = hipMallocAsync(reinterpret_cast<void**>(&t.d_u16), sizeof(uint16_t) * 4 * (size_t)n, s);
+        if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&t.d), sizeof(float4) * (size_t)n, s);
         if (e != hipSuccess) return fail_hip(ctx, e, what);
         t.capacity = n;
     }

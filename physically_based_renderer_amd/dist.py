@@ -100,16 +100,21 @@ def init_from_env(backend: str, always: bool = False, timeout: Optional[datetime
     return rank, world, local
 
 
-_gather_group = None
+_gather_group = None  # (the default group it was created under, the gather group)
 
 
 def gather_group():
-    """The process group the band gather runs on: every rank, with collective_timeout() (created once per
-    process, collectively: every rank calls it the first time it builds a BandGather). None at world 1."""
+    """The process group the band gather runs on: every rank, with collective_timeout() (created once per default
+    process group, collectively: every rank calls it the first time it builds a BandGather). None at world 1. The
+    cache is keyed on the default group object, so after destroy_process_group() and a new init_process_group() the
+    next BandGather builds a group of the new world instead of reusing one of the destroyed world."""
     global _gather_group
-    if _gather_group is None and dist.is_initialized() and dist.get_world_size() > 1:
-        _gather_group = dist.new_group(timeout=collective_timeout())
-    return _gather_group
+    if not dist.is_initialized() or dist.get_world_size() <= 1:
+        return None
+    world = dist.group.WORLD
+    if _gather_group is None or _gather_group[0] is not world:
+        _gather_group = (world, dist.new_group(timeout=collective_timeout()))
+    return _gather_group[1]
 
 
 class BandGather:

@@ -25,6 +25,45 @@ STRIDES = (216, 221)
 LAYOUTS = {"pair": {}, "px1": {"PBR_PIXELS_PER_THREAD": "1"}, "nolean": {"PBR_LEAN": "0"}}
 
 
+DEBUG_LIB = os.path.join(ROOT, "physically_based_renderer_amd", "_lib", "debug_bounds", "libpbrshade.so")
+DEBUG_FLAVOR = "debug_bounds"
+# The units `make debug-bounds` compiles with -DPBR_DEBUG_BOUNDS=1; the G-buffer fill is the product object (host code).
+DEBUG_UNITS = ("shade_kernels", "shade_kernels_bal", "pbr_context")
+
+
+def library_build_info(lib_path: str) -> dict:
+    """pbr_build_info of the library at `lib_path`, read in a child process (one libpbrshade.so per process; loading it
+    touches no GPU)."""
+    import json
+    import subprocess
+
+    code = ("import json, sys; sys.path.insert(0, %r); from physically_based_renderer_amd import _native as N; "
+            "print(json.dumps(N.build_info()))" % ROOT)
+    env = {**os.environ, "PBR_LIB_PATH": lib_path}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    if r.returncode != 0:
+        raise RuntimeError(f"cannot read the build info of {lib_path}: {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def debug_library_problems(info: dict, tree_sha: str) -> list:
+    """Why a library is not the bounds-checked build of this checkout (empty = it is): a unit stamped with other
+    sources than the checkout's (a stale `make debug-bounds`: round 5's pass-2 log compared such a library with the
+    product), or a kernel unit that is not a debug_bounds build (the product library, a variant)."""
+    bad = []
+    if not info.get("units"):
+        return ["the library reports no build info (ABI < 9)"]
+    for u in info["units"]:
+        if u["sources_sha"] != tree_sha:
+            bad.append(f"unit {u['unit']} built from sources {u['sources_sha']}, checkout is {tree_sha}")
+        if u["unit"] in DEBUG_UNITS and u["flavor"] != DEBUG_FLAVOR:
+            bad.append(f"unit {u['unit']} is a {u['flavor']!r} build, not {DEBUG_FLAVOR!r}")
+    missing = set(DEBUG_UNITS) - {u["unit"] for u in info["units"]}
+    if missing:
+        bad.append(f"units missing: {sorted(missing)}")
+    return bad
+
+
 def _cases():
     from physically_based_renderer_amd import _native as N
 

@@ -74,6 +74,35 @@ def test_pmc_lookup_is_keyed_by_workload_and_mode(tmp_path):
         assert (traffic == e["hbm_bytes_per_launch"]) if quoted else (traffic is None and prov["stale"])
 
 
+def test_roofline_block_names_its_unit_and_the_profiled_box():
+    """roofline: `bound` keeps the contract's vocabulary, `bound_unit` says which unit the roof is; `frac` from this
+    run's events, `frac_profile` from the committed profile's kernel-trace mean and `launch_vs_profile` the ratio --
+    only when the profile is of this build (stale: None)."""
+    pc3 = S.scene_pass(S.CONFIGS[3])
+    px = 3840 * 2160
+    fpp, bpp = bench.flops_per_pixel(pc3), bench.bytes_per_pixel(pc3)
+    stats = {"geometry_pixels": px, "light_terms": 32 * px, "backface_tests": 64 * px, "cull_tiles": 0,
+             "exact_pixels": 0}
+    prov = {"profile": "p", "kernel_sources_sha": "a", "profile_kernel_sources_sha": "a", "profile_kernel_mean_ms": 0.85}
+    r = bench.roofline_block(fpp, 3560.0, bpp, 60, px, 0.816e-3, 0.815, 5.16e8, 0.886, prov, "k", stats)
+    assert r["bound"] == "mfma" and r["bound_unit"] == "valu" and r["unit"] == "TFLOP/s"
+    assert r["frac"] == pytest.approx(fpp * px / 0.816e-3 / 1e12 / bench.FP32_PEAK_TFLOPS, abs=1e-4)
+    assert r["frac_profile"] == pytest.approx(fpp * px / 0.85e-3 / 1e12 / bench.FP32_PEAK_TFLOPS, abs=1e-4)
+    assert r["launch_vs_profile"] == pytest.approx(0.816 / 0.85, abs=1e-4)
+    r = bench.roofline_block(fpp, 3560.0, bpp, 60, px, 0.816e-3, 0.815, None, None, {**prov, "stale": True}, "k", stats)
+    assert r["frac_profile"] is None and r["launch_vs_profile"] is None
+    pc2 = S.scene_pass(S.CONFIGS[2])
+    f2, b2 = bench.flops_per_pixel(pc2), bench.bytes_per_pixel(pc2)
+    r = bench.roofline_block(f2, f2, b2, 60, 1920 * 1080, 51e-6, 0.051, None, None, prov, "k", stats)
+    assert r["bound"] == r["bound_unit"] == "hbm" and r["unit"] == "GB/s"
+    assert r["frac_profile"] == pytest.approx(b2 * 1920 * 1080 / 0.85e-3 / 1e9 / bench.HBM_PEAK_GBPS, abs=1e-5)
+    # the committed summary carries the profiled box's kernel mean for the headline workload
+    e = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))["cfg3_3840x2160_64pt_ibl_chelsea_faithful"]
+    _, _, p = bench.load_pmc("cfg3_3840x2160_64pt_ibl_chelsea_faithful", e["kernel_sources_sha"])
+    assert p["profile_kernel_mean_ms"] == round(e["kernel_trace"]["mean_ms_timed_steps"], 4)
+    assert bench.LINE_SCHEMA == 6
+
+
 def test_executed_flops_count_only_evaluated_terms():
     """frac_executed's model: per geometry pixel the fixed part, 91 / 74 FLOP per evaluated point / directional
     term, 8 per back-face test of the balanced lists, the range tests of culled passes."""

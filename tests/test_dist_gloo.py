@@ -82,6 +82,50 @@ def test_row_bands_gather_equals_single_frame(world, height):
     assert np.array_equal(frame.view(np.uint32), whole.view(np.uint32))
 
 
+def _reinit_worker(rank, world, inits, q):
+    """Two worlds in one process: init, gather, destroy_process_group, init again on a fresh store, gather again.
+    The gather group of the first world must not be reused by the second (dist.gather_group keys its cache on the
+    default group)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from physically_based_renderer_amd import dist as D
+
+    groups = []
+    for k, init in enumerate(inits):
+        os.environ.update(PBR_DIST_INIT_METHOD=init, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+        D.init_from_env("gloo")
+        band = D.band_rows(16, world, rank)
+        g = D.BandGather(band, 8, "cpu")
+        groups.append(g.group)
+        slot = torch.full((band.rows_max, 8, 4), float(10 * k + rank))
+        D.BandGather.wait(g.start(slot))
+        if rank == 0:
+            q.put((k, [float(g.frame[r, 0, 0, 0]) for r in range(world)]))
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        q.put(("distinct", groups[0] is not groups[1]))
+
+
+def test_gather_group_follows_a_reinitialised_world():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    tmp1, init1 = _rendezvous()
+    tmp2, init2 = _rendezvous()
+    with tmp1, tmp2:
+        procs = [ctx.Process(target=_reinit_worker, args=(r, 2, [init1, init2], q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        got = [q.get(timeout=240) for _ in range(3)]
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+    assert got == [(0, [0.0, 1.0]), (1, [10.0, 11.0]), ("distinct", True)]
+
+
 def _dead_peer_worker(rank, world, init, q, how):
     """Rank 1 joins the group and then dies (or hangs) before it sends its band; rank 0's gather must give up with
     GatherError -- at once for a lost connection, within the gather's timeout (PBR_DIST_TIMEOUT_S, here 4 s) for a

@@ -19,12 +19,19 @@ import bounds_cases
 pytestmark = pytest.mark.gpu
 
 ROOT = bounds_cases.ROOT
-DEBUG_LIB = os.path.join(ROOT, "physically_based_renderer_amd", "_lib", "debug_bounds", "libpbrshade.so")
+DEBUG_LIB = bounds_cases.DEBUG_LIB
 
 
 def _child(tmp_path, name, extra_env=None):
+    from physically_based_renderer_amd import _native as N
+
     if not os.path.exists(DEBUG_LIB):
         pytest.fail(f"{DEBUG_LIB} missing: run `make -C physically_based_renderer_amd/csrc debug-bounds` first")
+    # Which library the comparison runs: the bounds-checked build of THIS checkout, or the test stops here (a stale
+    # debug build and a real debug/product divergence would otherwise look the same).
+    problems = bounds_cases.debug_library_problems(bounds_cases.library_build_info(DEBUG_LIB), N.kernel_sources_sha())
+    assert not problems, (f"{DEBUG_LIB} is not the bounds-checked build of this checkout: " + "; ".join(problems)
+                          + " (rebuild: make -C physically_based_renderer_amd/csrc debug-bounds)")
     out = tmp_path / f"{name}.npz"
     env = {**os.environ, "PBR_LIB_PATH": DEBUG_LIB, **(extra_env or {})}
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "bounds_cases.py"), str(out)], env=env,

@@ -95,6 +95,43 @@ def test_set_pass_on_one_stream_shade_on_another(gpu, env_map):
         assert O.bit_equal(out.cpu().numpy(), want_b).all()
 
 
+def test_grow_a_slot_and_the_env_map_while_another_stream_reads_them(gpu, env_map):
+    """Stream 0 queues eight passes reading light slot 0 and the environment map; stream 1 then cycles the ring back
+    to slot 0 with more lights than it holds and uploads a larger environment map -- both grow -- and shades. The
+    old buffers are released in stream order after stream 0's passes (free_after_readers: stream-side event waits,
+    hipFreeAsync; no device synchronisation), so every stream-0 frame still carries the bits of pass A shaded alone
+    and stream 1's frame those of the grown pass."""
+    planes, pa, _ = _two_passes()
+    gb = GBuffer.from_host(planes, gpu)
+    rng = np.random.default_rng(11)
+    more = np.concatenate([pa.light_array()] * 3)[:150].copy()  # 150 lights: past the slot's 64
+    more[:, 8:11] = rng.uniform(-20, 20, (150, 3))
+    pc_big = _with(pa, num_point_lights=150, lights_array=more)
+    env_big = np.ascontiguousarray(np.tile(env_map, (2, 2, 1)))
+    with ShadingContext(0) as fresh:
+        want_a, _ = _solo(fresh, gb, pa, env_map)
+        want_big, _ = _solo(fresh, gb, pc_big, env_big)
+    with ShadingContext(0) as ctx:
+        s0, s1 = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+        outs = [torch.empty((gb.height, gb.width, 4), dtype=torch.float32, device=gpu) for _ in range(8)]
+        out = torch.empty_like(outs[0])
+        ctx.set_pass(pa, stream=s1)  # slot 0
+        ctx.set_env_map(env_map, stream=s1)
+        ctx.shade(gb, out, stream=s1)  # stream 1 known to the context before stream 0's passes queue
+        torch.cuda.synchronize()
+        for o in outs:
+            ctx.shade(gb, o, stream=s0)
+        for _ in range(3):  # slots 1-3
+            ctx.set_pass(pa, stream=s1)
+        ctx.set_pass(pc_big, stream=s1)  # slot 0 again: grows while stream 0 may still read it
+        ctx.set_env_map(env_big, stream=s1)  # grows the texture stream 0 reads
+        ctx.shade(gb, out, stream=s1)
+        torch.cuda.synchronize()
+        bad = [k for k, o in enumerate(outs) if not O.bit_equal(o.cpu().numpy(), want_a).all()]
+        assert not bad, f"stream-0 frames {bad} differ from pass A shaded alone"
+        assert O.bit_equal(out.cpu().numpy(), want_big).all()
+
+
 def _host_dots(planes, lights):
     """(N . l, |N|_1 |l|_1) per (pixel, point light) in fp64, l = light position - P."""
     p = planes[0:3].reshape(3, -1).T.astype(np.float64)
@@ -228,7 +265,7 @@ def test_grow_resources_after_a_reader_stream_is_destroyed(first, gpu, env_map):
     """A pass on a caller-created stream S, S destroyed once its passes finished (the contract, pbr_shade.h), then
     the context's resources grow past their capacity -- more lights than the slot S read held (the ring's four slots
     cycled back to it), a larger environment map: the frees before the growth must not touch S's dead handle
-    (pbr_context.hip before_free synchronises the device instead), and the next pass carries the bits of the same
+    (pbr_context.hip free_after_readers orders them on the growing stream with events), and the next pass carries the bits of the same
     pass on a fresh context. `first`: which resource grows first (the first growth meets S's record)."""
     import ctypes
 

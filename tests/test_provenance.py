@@ -91,6 +91,32 @@ def test_bench_refuses_a_variant_or_stale_library(kind, tmp_path):
     assert r.returncode != bench.EXIT_PROVENANCE and "REFUSED" not in r.stderr
 
 
+def test_debug_bounds_comparison_refuses_a_restamped_or_product_library(tmp_path):
+    """tests/test_gpu_debug_bounds.py compares frames only after checking WHICH library its child loads: every unit
+    stamped with this checkout's sources and the kernel units built as debug_bounds. A library with one unit restamped
+    (a stale `make debug-bounds`) and the product library are both refused, with the reason named; the in-tree debug
+    library passes when it is present and current."""
+    import bounds_cases as B
+
+    tree = N.kernel_sources_sha()
+    stale = _relink(tmp_path, "stale_dbg", ['-DPBR_SOURCES_SHA="0123456789abcdef"', '-DPBR_BUILD_FLAVOR="product"'])
+    p = B.debug_library_problems(B.library_build_info(stale), tree)
+    assert any("unit gbuffer_fill built from sources 0123456789abcdef" in s for s in p), p
+    assert any("is a 'product' build, not 'debug_bounds'" in s for s in p), p
+    p = B.debug_library_problems(B.library_build_info(N.LIB_PATH), tree)
+    assert p and all("'product' build" in s for s in p), p
+    assert B.debug_library_problems({"units": []}, tree)
+    # a debug library whose kernel units carry an older stamp (the round-5 failure's cause, DESIGN.md 5d)
+    info = {"units": [{"unit": u, "sources_sha": "ffffffffffffffff", "flavor": B.DEBUG_FLAVOR} for u in B.DEBUG_UNITS]
+            + [{"unit": "gbuffer_fill", "sources_sha": tree, "flavor": "product"}]}
+    p = B.debug_library_problems(info, tree)
+    assert len(p) == 3 and all("ffffffffffffffff" in s for s in p)
+    if os.path.exists(B.DEBUG_LIB):
+        info = B.library_build_info(B.DEBUG_LIB)
+        if info["sources_sha"] == tree or all(u["sources_sha"] == tree for u in info["units"]):
+            assert B.debug_library_problems(info, tree) == []
+
+
 def test_bench_records_the_loaded_library():
     """library_provenance describes the loaded build in the line (path, stamp, flavor, units) and lists problems."""
     lib = bench.library_provenance(False)
