@@ -144,14 +144,41 @@ __device__ __forceinline__ ItemPixel item_pixel(const PixelInvariants2& q, const
     return r;
 }
 
+// A record's dwords go to LDS two at a time from wherever they sit in registers (ds_write2_b32): as float4 stores the
+// compiler first assembled each quad in four consecutive VGPRs -- ~20 v_mov per record, four records per lane (rank
+// phase). `dw` counts dwords from `dst`. Inline asm with a memory clobber: the LDS instructions of one wave execute in
+// order, so the loads after the wave_lds_sync that follows see the data.
+template <int DW>
+__device__ __forceinline__ void lds_write2(uint32_t addr, float a, float b) {
+    static_assert(DW >= 0 && DW + 1 <= 255, "ds_write2_b32 offsets are 8-bit dword counts");
+    asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(addr), "v"(a), "v"(b), "i"(DW), "i"(DW + 1)
+                 : "memory");
+}
+template <int DW>
+__device__ __forceinline__ void lds_write1(uint32_t addr, float a) {
+    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "v"(a), "i"(4 * DW) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    typedef __attribute__((address_space(3))) const char lds_char;
+    return (uint32_t)(uintptr_t)(const lds_char*)p;
+}
+
+// The faithful record: the float4 layout load_item reads (dwords 0-25; 26, 27 unused).
 __device__ __forceinline__ void store_item(float4* dst, const ItemPixel& p) {
-    dst[0] = make_float4(p.pos.x, p.pos.y, p.pos.z, p.n.x);
-    dst[1] = make_float4(p.n.y, p.n.z, p.v.x, p.v.y);
-    dst[2] = make_float4(p.v.z, p.f0.x, p.f0.y, p.f0.z);
-    dst[3] = make_float4(p.omf0.x, p.omf0.y, p.omf0.z, p.mab.x);
-    dst[4] = make_float4(p.mab.y, p.mab.z, p.a2m1, p.k);
-    dst[5] = make_float4(p.omk, p.nv, p.a2gv, __uint_as_float(p.live0));
-    dst[6] = make_float4(__uint_as_float(p.live1), __int_as_float(p.origin), 0.0f, 0.0f);
+    const uint32_t a = lds_addr(dst);
+    lds_write2<0>(a, p.pos.x, p.pos.y);
+    lds_write2<2>(a, p.pos.z, p.n.x);
+    lds_write2<4>(a, p.n.y, p.n.z);
+    lds_write2<6>(a, p.v.x, p.v.y);
+    lds_write2<8>(a, p.v.z, p.f0.x);
+    lds_write2<10>(a, p.f0.y, p.f0.z);
+    lds_write2<12>(a, p.omf0.x, p.omf0.y);
+    lds_write2<14>(a, p.omf0.z, p.mab.x);
+    lds_write2<16>(a, p.mab.y, p.mab.z);
+    lds_write2<18>(a, p.a2m1, p.k);
+    lds_write2<20>(a, p.omk, p.nv);
+    lds_write2<22>(a, p.a2gv, __uint_as_float(p.live0));
+    lds_write2<24>(a, __uint_as_float(p.live1), __int_as_float(p.origin));
 }
 __device__ __forceinline__ ItemPixel load_item(const float4* src) {
     const float4 a = src[0], b = src[1], c = src[2], d = src[3], e = src[4], f = src[5], g = src[6];
@@ -204,13 +231,21 @@ __device__ __forceinline__ ItemPixelX item_pixel_x(const PixelInvariants2& q, co
     return r;
 }
 
+// The exact record: the float4 layout load_item_x reads (dwords 0-22; 23 unused).
 __device__ __forceinline__ void store_item(float4* dst, const ItemPixelX& p) {
-    dst[0] = make_float4(p.pos.x, p.pos.y, p.pos.z, p.n.x);
-    dst[1] = make_float4(p.n.y, p.n.z, p.v.x, p.v.y);
-    dst[2] = make_float4(p.v.z, p.albedo.x, p.albedo.y, p.albedo.z);
-    dst[3] = make_float4(p.f0.x, p.f0.y, p.f0.z, p.omm);
-    dst[4] = make_float4(p.a_sqr, p.k, p.ggx_v, p.nv4);
-    dst[5] = make_float4(__uint_as_float(p.live0), __uint_as_float(p.live1), __int_as_float(p.origin), 0.0f);
+    const uint32_t a = lds_addr(dst);
+    lds_write2<0>(a, p.pos.x, p.pos.y);
+    lds_write2<2>(a, p.pos.z, p.n.x);
+    lds_write2<4>(a, p.n.y, p.n.z);
+    lds_write2<6>(a, p.v.x, p.v.y);
+    lds_write2<8>(a, p.v.z, p.albedo.x);
+    lds_write2<10>(a, p.albedo.y, p.albedo.z);
+    lds_write2<12>(a, p.f0.x, p.f0.y);
+    lds_write2<14>(a, p.f0.z, p.omm);
+    lds_write2<16>(a, p.a_sqr, p.k);
+    lds_write2<18>(a, p.ggx_v, p.nv4);
+    lds_write2<20>(a, __uint_as_float(p.live0), __uint_as_float(p.live1));
+    lds_write1<22>(a, __int_as_float(p.origin));
 }
 __device__ __forceinline__ ItemPixelX load_item_x(const float4* src) {
     const float4 a = src[0], b = src[1], c = src[2], d = src[3], e = src[4], f = src[5];
@@ -249,8 +284,31 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ float bal_wave_min(float v) { return wave_min_dpp(v); }
-__device__ __forceinline__ float bal_wave_max(float v) { return wave_max_dpp(v); }
+// Pass 1 runs in fast-window waves only (lean and faithful or exact lean: every position |x| <= 2^20, every light inside
+// its window), so every value it reduces is finite: the float-unit reductions (wave_minmax_finite).
+// FINITE: the faithful kernel's pass 1. The exact balanced kernel keeps the order-key reductions (wave_min_dpp): with
+// the float-unit ones its SGPR spills to VGPR lanes grew (295 -> 361 lane moves in the kernel) and config 3 exact
+// measured ~1% slower.
+template <bool FINITE>
+__device__ __forceinline__ float bal_wave_min(float v) {
+    if constexpr (FINITE) return wave_min_finite(v);
+    else return wave_min_dpp(v);
+}
+template <bool FINITE>
+__device__ __forceinline__ float bal_wave_max(float v) {
+    if constexpr (FINITE) return wave_max_finite(v);
+    else return wave_max_dpp(v);
+}
+template <bool FINITE>
+__device__ __forceinline__ float bal_fmin(float a, float b) {
+    if constexpr (FINITE) return fmin_finite(a, b);
+    else return fminf(a, b);
+}
+template <bool FINITE>
+__device__ __forceinline__ float bal_fmax(float a, float b) {
+    if constexpr (FINITE) return fmax_finite(a, b);
+    else return fmaxf(a, b);
+}
 
 // Pass 1 for the pair and four lights j..j+3 (coordinates x, y, z: one float4 per axis, light j + i in element i):
 // shift the lights' SKIP bits for each pixel (the sign of t1, see the header comment) into `ma` / `mb`, light j + 3
@@ -319,13 +377,23 @@ __device__ __forceinline__ void read_pair_lights(const float* lds_lights, int j0
 // LightingUtil.hlsl:131: pass 1 removed every item whose light is beyond the range of its pixel (balanced_pass1), so
 // each item here is within range and the 0/1 factor in_range01 would be exactly 1 (the sentinel's zero strength
 // still zeroes its term).
+// The two rare cases of an item share one test: |V + L| (the length normalize(V + L) divides by) below kBalNearVL.
+// Unit V and L give H.V = |V + L| / 2 (with |V|, |L| = 1 within a few 2^-24, H.V >= |V + L| / 2 - 2^-21 / |V + L| after
+// the roundings), so |V + L| >= 1/16 gives H.V > 0.0312 and x = 1 - H.V < 0.9688: below pow5_fast3's glibc band
+// (x > 0.97), and far above normalize_x2's window (|V + L| >= 2^-30). Only when a live lane's item falls below 1/16 (L
+// within ~3.6 degrees of -V: rare, as the glibc band is) does the wave run the window test and the band patch, as a
+// uniform branch: 2 compares per iteration instead of 4.
+constexpr float kBalNearVL = 0.0625f;
 __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const f3x2& lp, const f3x2& ls, m2& ok,
                                                       f3x2& sum, uint64_t live) {
     f3x2 l = f3x2{lp.x - q.pos.x, lp.y - q.pos.y, lp.z - q.pos.z};
     const v2 dist = sqrt_nr(dot3(l, l));  // >= 0.01 for a live item of a pixel pass 1 did not redo
     const Recip2 rdist = recip_nr(dist);
     l = f3x2{div_nr(l.x, rdist), div_nr(l.y, rdist), div_nr(l.z, rdist)};
-    const f3x2 h = normalize_x2(f3x2{q.v.x + l.x, q.v.y + l.y, q.v.z + l.z}, ok);
+    const f3x2 vl = f3x2{q.v.x + l.x, q.v.y + l.y, q.v.z + l.z};
+    const v2 svl = sqrt_nr(dot3(vl, vl));  // normalize_x2's operations, its window test below
+    const Recip2 rvl = recip_nr(svl);
+    const f3x2 h = f3x2{div_nr(vl.x, rvl), div_nr(vl.y, rvl), div_nr(vl.z, rvl)};
     const v2 att = rdist.r * rdist.r;
     const f3x2 n = splat3(q.n.x, q.n.y, q.n.z);
     const v2 n_dot_h = dot3_sat(n, h);
@@ -333,7 +401,15 @@ __device__ __forceinline__ void faithful_point_items2(const ItemPixel& q, const 
     const v2 den = inner * inner;
     const v2 n_dot_l = dot3_sat(n, l);
     const v2 r = rcp_hw((den * vfma(n_dot_l, splat(q.omk), splat(q.k))) * vfma(splat(q.nv), n_dot_l, splat(0.001f)));
-    const v2 p = pow5_fast3(1.0f - dot3_sat(h, splat3(q.v.x, q.v.y, q.v.z)), live);
+    const v2 x = 1.0f - dot3_sat(h, splat3(q.v.x, q.v.y, q.v.z));
+    const v2 x2 = x * x;
+    const v2 x4 = x2 * x2;
+    v2 p = x4 * x;  // pow5_fast3's products
+    if (__builtin_expect(((lanes(svl.x < kBalNearVL) | lanes(svl.y < kBalNearVL)) & live) != 0, 0)) {
+        ok &= ge(svl, 0x1p-30f);  // normalize_x2's window
+        if (x.x > PBR_POW5_FAST3_GLIBC_FROM && on(live)) p.x = pow5_glibc(x.x);  // pow5_fast3's band
+        if (x.y > PBR_POW5_FAST3_GLIBC_FROM && on(live)) p.y = pow5_glibc(x.y);
+    }
     const f3x2 f = f3x2{q.f0.x + q.omf0.x * p, q.f0.y + q.omf0.y * p, q.f0.z + q.omf0.z * p};
     const v2 kr = (q.a2gv * n_dot_l) * r;
     const v2 w = att * n_dot_l;
@@ -406,6 +482,7 @@ __device__ __forceinline__ m2 beyond_range(const f3x2& pos, float lx, float ly, 
 // roundings) needs no test; for another (rare) light each pixel whose live mask holds it runs the item's own test --
 // the same dist from the same operations -- and a pixel that fails is redone on the exact path (near_a / near_b), as
 // a failed window test in pass 2 would have redone it.
+template <bool EXACT>
 __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& n, bool live_a, bool live_b, int nl,
                                                    float dist_lo, BalancedWaveLds& w, const float* lds_lights,
                                                    unsigned long long* bal_prof = nullptr) {
@@ -417,17 +494,18 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
     // the wave (the extra terms cover the roundings of c, r and B_k) into the wave's LDS region.
     const float big = 3.0e38f;
     const f3 pa = lane(pos, 0), pb = lane(pos, 1);
-    const float mnx = bal_wave_min(fminf(live_a ? pa.x : big, live_b ? pb.x : big));
-    const float mny = bal_wave_min(fminf(live_a ? pa.y : big, live_b ? pb.y : big));
-    const float mnz = bal_wave_min(fminf(live_a ? pa.z : big, live_b ? pb.z : big));
-    const float mxx = bal_wave_max(fmaxf(live_a ? pa.x : -big, live_b ? pb.x : -big));
-    const float mxy = bal_wave_max(fmaxf(live_a ? pa.y : -big, live_b ? pb.y : -big));
-    const float mxz = bal_wave_max(fmaxf(live_a ? pa.z : -big, live_b ? pb.z : -big));
+    constexpr bool F = !EXACT;
+    const float mnx = bal_wave_min<F>(bal_fmin<F>(live_a ? pa.x : big, live_b ? pb.x : big));
+    const float mny = bal_wave_min<F>(bal_fmin<F>(live_a ? pa.y : big, live_b ? pb.y : big));
+    const float mnz = bal_wave_min<F>(bal_fmin<F>(live_a ? pa.z : big, live_b ? pb.z : big));
+    const float mxx = bal_wave_max<F>(bal_fmax<F>(live_a ? pa.x : -big, live_b ? pb.x : -big));
+    const float mxy = bal_wave_max<F>(bal_fmax<F>(live_a ? pa.y : -big, live_b ? pb.y : -big));
+    const float mxz = bal_wave_max<F>(bal_fmax<F>(live_a ? pa.z : -big, live_b ? pb.z : -big));
     const float cx = 0.5f * mnx + 0.5f * mxx, cy = 0.5f * mny + 0.5f * mxy, cz = 0.5f * mnz + 0.5f * mxz;
     const float r = (0.5f * (mxx - mnx) + 0.5f * (mxy - mny)) + 0.5f * (mxz - mnz);
     const float slack = r + (fabsf(cx) + fabsf(cy) + fabsf(cz)) * 0x1p-22f;
-    const float pmax = bal_wave_max(fmaxf(live_a ? (fabsf(pa.x) + fabsf(pa.y)) + fabsf(pa.z) : 0.0f,
-                                          live_b ? (fabsf(pb.x) + fabsf(pb.y)) + fabsf(pb.z) : 0.0f));
+    const float pmax = bal_wave_max<F>(bal_fmax<F>(live_a ? (fabsf(pa.x) + fabsf(pa.y)) + fabsf(pa.z) : 0.0f,
+                                                   live_b ? (fabsf(pb.x) + fabsf(pb.y)) + fabsf(pb.z) : 0.0f));
     float bj = 0.0f;  // B_j of light j = lane (j < nl; padded lights: zero position, harmless), B = the maximum
     bool near = true, far = false;  // light j: within range of every pixel of the box / beyond range of every one
     bool close = false;             // light j may come closer than dist_lo to a pixel of the box (or is NaN)
@@ -449,7 +527,7 @@ __device__ __forceinline__ BalMasks balanced_pass1(const f3x2& pos, const f3x2& 
         far = (gx * gx + gy * gy) + gz * gz >= 100.1f * 100.1f;
         close = !((gx * gx + gy * gy) + gz * gz >= (1.02f * dist_lo) * (1.02f * dist_lo));
     }
-    const float bmax = bal_wave_max(bj);
+    const float bmax = bal_wave_max<F>(bj);
     const uint64_t far_m = lanes(far), cross_m = lanes(!near && !far), close_m = lanes(close);  // bit j: light j
     const v2 cn = v2{0x1p-18f * ((fabsf(n.x.x) + fabsf(n.y.x)) + fabsf(n.z.x)),
                      0x1p-18f * ((fabsf(n.x.y) + fabsf(n.y.y)) + fabsf(n.z.y))};
@@ -553,6 +631,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     redo |= mask2(bm.near_a, bm.near_b);  // pass 1's distance window (the items carry no test)
     constexpr int R = EXACT ? kBalRecX : kBalRec;  // record stride (float4)
     BAL_PROF_T(t1);
+    PBR_PHASE("rank");
 
     // ---- rank the wave's 128 pixels by live count (counting sort; ties in LDS-atomic order, which only
     // decides which lane evaluates a pixel, never how)
@@ -591,6 +670,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     wave_lds_sync();
 
     BAL_PROF_T(t2);
+    PBR_PHASE("pass2");
     // ---- pass 2
     // Every lane runs every iteration (no divergent body): a lane with no live light left takes the zero sentinel
     // (index kBalMaxLights: position and strength 0) for both elements, whose terms its dead accumulator absorbs.
@@ -683,6 +763,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
         }
     }
     BAL_PROF_T(t3);
+    PBR_PHASE("handback");
     // ---- hand the results back: the owner reads its two pixels' (by origin 2 lane + element)
     wave_lds_sync();
     const float2 rx = reinterpret_cast<const float2*>(w.start[0])[lane_id];

@@ -11,6 +11,7 @@
 #include "libm_f32.h"
 #include "libm_f32_x2.h"
 #include "pbr_debug_bounds.h"
+#include "pbr_census.h"
 
 namespace pbr {
 
@@ -383,6 +384,7 @@ __device__ __forceinline__ int wrap_index(float f, int n) {
         const int j = i < 0 ? i + n : i;
         return j >= n ? j - n : j;                     // == ((i % n) + n) % n on this range
     }
+    PBR_COLD("wrap_mod");
     const int m = i % n;
     return m < 0 ? m + n : m;
 }

@@ -62,6 +62,52 @@ __device__ __forceinline__ float wave_minmax_dpp(float v, float neutral) {
 }
 __device__ __forceinline__ float wave_min_dpp(float v, float neutral = 3.0e38f) { return wave_minmax_dpp<false>(v, neutral); }
 __device__ __forceinline__ float wave_max_dpp(float v, float neutral = -3.0e38f) { return wave_minmax_dpp<true>(v, neutral); }
+// Min / max over the wave of FINITE floats (the balanced pass-1 box of a fast-window wave: every position and bound is
+// finite there), on the float unit: v_min_f32_dpp / v_max_f32_dpp through the four in-row steps, then row_bcast 15 / 31
+// carry the row results up (rows 1, 3, then 2, 3), so lane 63 holds the wave's result: one v_readlane. No order key, no
+// NaN mapping, no scalar combine of four row results (which needed VGPR moves for its three-operand form): 6 DPP
+// instructions and a readlane instead of ~17 VALU. Inline asm with the two wait states a DPP read of a VGPR written by
+// the previous VALU instruction needs (s_nop 1); every lane must be active. -0 and +0 may come out either way (IEEE
+// minNum), which changes nothing computed from a bound.
+template <bool MAX>
+__device__ __forceinline__ float wave_minmax_finite(float v) {
+    if constexpr (MAX) {
+        asm volatile(
+            "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+            "s_nop 1"
+            : "+v"(v));
+    } else {
+        asm volatile(
+            "s_nop 1\n\tv_min_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+            "s_nop 1\n\tv_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+            "s_nop 1"
+            : "+v"(v));
+    }
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+__device__ __forceinline__ float wave_min_finite(float v) { return wave_minmax_finite<false>(v); }
+__device__ __forceinline__ float wave_max_finite(float v) { return wave_minmax_finite<true>(v); }
+// fminf / fmaxf of finite operands as one instruction (the compiler quiets operands it cannot prove canonical with an
+// extra v_max each, as IEEE mode requires for a possible signalling NaN; none reaches these).
+__device__ __forceinline__ float fmin_finite(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float fmax_finite(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 // Sum over the wave, wave-uniform.
 __device__ __forceinline__ int wave_sum_dpp(int v) {
     v += dpp_row_move<0xB1>(v);
@@ -163,6 +209,7 @@ struct PixelInvariants2 {
 // division, GeometrySchlickGGX(N.V) = n_dot_v / (n_dot_v (1-k) + k), takes the Markstein step for
 // pixels in the fast window (`fast`): roughness in [0, 1] puts k in [1/8, 1/2] and the denominator in
 // [2^-3, 2^5]; n_dot_v must be 0 or >= 2^-100 so the residual stays normal. Otherwise IEEE.
+__device__ __forceinline__ PixelInvariants2 complete_invariants(PixelInvariants2 q, v2 roughness, m2 fast);
 __device__ __forceinline__ PixelInvariants2 make_invariants(const f3x2& n, const f3x2& v, const f3x2& albedo,
                                                             const f3x2& f0, v2 metallic, v2 roughness, m2 fast) {
     PixelInvariants2 q;
@@ -172,6 +219,11 @@ __device__ __forceinline__ PixelInvariants2 make_invariants(const f3x2& n, const
     q.f0 = f0;
     q.one_minus_f0 = f3x2{1.0f - f0.x, 1.0f - f0.y, 1.0f - f0.z};
     q.one_minus_metal = 1.0f - metallic;
+    return complete_invariants(q, roughness, fast);
+}
+// make_invariants' light-loop fields (a^2, k, GeometrySchlickGGX(N.V), 4 N.V) from q's N and V and the roughness.
+__device__ __forceinline__ PixelInvariants2 complete_invariants(PixelInvariants2 q, v2 roughness, m2 fast) {
+    const f3x2 n = q.n, v = q.v, f0 = q.f0;
     v2 r = vmax(roughness, splat(0.05f));
     v2 a = r * r;
     q.a_sqr = a * a;
@@ -191,6 +243,21 @@ __device__ __forceinline__ PixelInvariants2 make_invariants(const f3x2& n, const
     q.four_n_dot_v = 4.0f * n_dot_v;
     q.f0_nonzero = mask2(f0.x.x != 0.0f && f0.y.x != 0.0f && f0.z.x != 0.0f,
                          f0.x.y != 0.0f && f0.y.y != 0.0f && f0.z.y != 0.0f);
+    return q;
+}
+
+// The fields of make_invariants the finish reads (Default.hlsl:139-150: the ambient's N, V, F0, 1 - F0, 1 - metallic,
+// albedo), by the same operations, so the same bits; the light-loop fields (a^2, k, GeometrySchlickGGX(N.V), 4 N.V)
+// are left zero. The wave-balanced kernels form these after their loop; the rare exact re-pass forms the full set.
+__device__ __forceinline__ PixelInvariants2 make_finish_invariants(const f3x2& n, const f3x2& v, const f3x2& albedo,
+                                                                   const f3x2& f0, v2 metallic) {
+    PixelInvariants2 q{};
+    q.n = n;
+    q.v = v;
+    q.albedo = albedo;
+    q.f0 = f0;
+    q.one_minus_f0 = f3x2{1.0f - f0.x, 1.0f - f0.y, 1.0f - f0.z};
+    q.one_minus_metal = 1.0f - metallic;
     return q;
 }
 

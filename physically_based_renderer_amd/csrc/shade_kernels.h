@@ -5,6 +5,8 @@
 #include <cstdint>
 #include <string>
 
+#include "pbr_census.h"
+
 namespace pbr {
 
 constexpr int kAmbientConstant = 0;

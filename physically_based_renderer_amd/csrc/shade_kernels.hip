@@ -280,6 +280,7 @@ __device__ __forceinline__ f3x2 lighting_fast(const PixelInvariants2& q, const f
     // out there, it was the register peak of that path.
     const int n_dir = BALANCED && !FAITHFUL ? 0 : ps.n_dir;
     for (int j = 0; j < n_dir; ++j) {  // directional: never culled
+        PBR_COLD("directional");
         const LightRec r = light_rec(lights, j, ps);
         m2 ok = fast_ok & light_flag(r);
         if (FAITHFUL) {
@@ -452,6 +453,7 @@ __device__ __forceinline__ PairIn load_pair(const GBufferArgs& gb, const PassArg
             v[i] = v2{t.x, t.y};
         }
     } else {
+        PBR_COLD("scalar_loads");
         ia = PBR_BOUNDS_PIXEL(ia, gb.width, gb.height, gb.row_stride, 1, kBoundsGBuffer);
         ib = PBR_BOUNDS_PIXEL(ib, gb.width, gb.height, gb.row_stride, 1, kBoundsGBuffer);
 #pragma unroll
@@ -498,16 +500,24 @@ __device__ __forceinline__ void launder(f3x2& x) {
 // V = normalize(g_CameraPosW - pin.PosW) (Default.hlsl:53) and the BRDF invariants of the pair. In the window
 // every component of eye - pos is 0 or >= 2^-44 and |eye - pos| < 2^22, so the exact fast normalize applies
 // once |V| >= 2^-30; other pixels take the IEEE sequences.
-__device__ __forceinline__ PixelInvariants2 pair_invariants(const PairIn& p, const PassArgs& ps, m2 fast2) {
+__device__ __forceinline__ f3x2 pair_view(const PairIn& p, const PassArgs& ps, m2 fast2) {
     const f3x2 ve = f3x2{ps.eye[0] - p.pos.x, ps.eye[1] - p.pos.y, ps.eye[2] - p.pos.z};
     m2 okv = fast2;
     f3x2 v = normalize_x2(ve, okv);
     const bool va_ok = on(okv.x), vb_ok = on(okv.y);
     if (__builtin_expect(!(va_ok && vb_ok), 0)) {
+        PBR_COLD("v_ieee");
         const f3 v0 = va_ok ? lane(v, 0) : normalize3(lane(ve, 0)), v1 = vb_ok ? lane(v, 1) : normalize3(lane(ve, 1));
         v = f3x2{v2{v0.x, v1.x}, v2{v0.y, v1.y}, v2{v0.z, v1.z}};
     }
-    return make_invariants(p.n, v, p.albedo, p.f0, p.metallic, p.roughness, fast2);
+    return v;
+}
+__device__ __forceinline__ PixelInvariants2 pair_invariants(const PairIn& p, const PassArgs& ps, m2 fast2) {
+    return make_invariants(p.n, pair_view(p, ps, fast2), p.albedo, p.f0, p.metallic, p.roughness, fast2);
+}
+// Only what the finish reads (make_finish_invariants): the wave-balanced kernels after their light loop.
+[[maybe_unused]] __device__ __forceinline__ PixelInvariants2 pair_finish_invariants(const PairIn& p, const PassArgs& ps, m2 fast2) {
+    return make_finish_invariants(p.n, pair_view(p, ps, fast2), p.albedo, p.f0, p.metallic);
 }
 
 // Ambient + tonemap + gamma for one pixel (Default.hlsl:139-160), returns the output RGBA.
@@ -564,6 +574,7 @@ __device__ __forceinline__ f3x2 ambient_ibl_pair(const PixelInvariants2& q, cons
     v2 uy = pbr_asinf_x2(q.n.y, sb);
     const bool spec_a = live_a && (sa[0] | sb[0]), spec_b = live_b && (sa[1] | sb[1]);
     if (__builtin_expect(lanes(spec_a || spec_b) != 0, 0)) {
+        PBR_COLD("ibl_special");
         if (spec_a) {
             ux.x = pbr_atan2f(q.n.z.x, q.n.x.x);
             uy.x = pbr_asinf(q.n.y.x);
@@ -606,6 +617,7 @@ __device__ __forceinline__ float4 finish_lit(f3 ambient, float ao, f3 direct, co
         return make_float4(pow_inv_gamma_faithful(lit.x), pow_inv_gamma_faithful(lit.y),
                            pow_inv_gamma_faithful(lit.z), ps.opacity);
     }
+    PBR_COLD("exact_finish");
     lit = mk3(reinhard(lit.x, fast), reinhard(lit.y, fast), reinhard(lit.z, fast));  // Default.hlsl:153
     return make_float4(pow_inv_gamma(lit.x), pow_inv_gamma(lit.y), pow_inv_gamma(lit.z),
                        ps.opacity);
@@ -618,7 +630,9 @@ __device__ __forceinline__ void finish_pair(const PixelInvariants2& q2, const Pi
                                             bool fast_b, bool faithful, bool live_a, bool live_b, float4& ca,
                                             float4& cb) {
     if constexpr (AMBIENT == kAmbientIblDiffuse) {
+        PBR_PHASE("ibl");
         const f3x2 amb = ambient_ibl_pair(q2, ps, env, faithful, live_a, live_b);
+        PBR_PHASE("finish");
         if (live_a) ca = finish_lit<APPLY_AO>(lane(amb, 0), ao_a, da, ps, fast_a, faithful);
         if (live_b) cb = finish_lit<APPLY_AO>(lane(amb, 1), ao_b, db, ps, fast_b, faithful);
     } else {
@@ -648,6 +662,7 @@ __device__ __forceinline__ float4 sky_finish(f3 col, bool fast) {
                        1.0f);
 }
 __device__ __forceinline__ float4 sky_pixel(f3 dir, const PassArgs& ps, const float4* __restrict__ sky, bool fast) {
+    PBR_COLD("sky");
     return sky_finish(sky_colour(dir, ps, sky), fast);
 }
 
@@ -687,6 +702,7 @@ __device__ __forceinline__ void alpha_keep_pair(const GBufferArgs& gb, int64_t g
                                                 float4& cb, bool& keep_a, bool& keep_b) {
     keep_a = keep_b = true;
     if (__builtin_expect(gb.alpha_test, 0)) {
+        PBR_COLD("alpha");
         if (ga) keep_a = alpha_keep(gb, grow, ca);
         if (gb_) keep_b = alpha_keep(gb, grow + 1, cb);
     }
@@ -837,6 +853,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                             bool exact_only) {
     __shared__ Lds s;
     TL_BEGIN();
+    PBR_PHASE("entry");
 #if PBR_BAL_PROFILE
     const long long t_entry = (long long)__builtin_amdgcn_s_memtime();
     unsigned long long* bal_prof = s.prof[__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6];
@@ -845,6 +862,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     load_libm_tables<AMBIENT == kAmbientIblDiffuse>();  // powf (+ atanf with IBL) tables -> LDS (pbr_device_math.h)
     if constexpr (BAL != 0) stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light);
     __syncthreads();
+    PBR_PHASE("load_window");
 
     const int tid = threadIdx.x;
     const int wave_id = __builtin_amdgcn_readfirstlane(tid) >> 6;  // wave-uniform (SGPR)
@@ -905,6 +923,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     f3x2 pos2 = p.pos;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
     bool faithful_wave = false;  // wave-uniform: the faithful loop ran, so the finish may be faithful too
+    bool finish_q2_only = false;  // wave-uniform: q2 holds only the finish's fields (the wave-balanced paths)
+    v2 rough2 = splat(0.0f);      // ... and then the pair's roughness, for the exact re-pass's full set
     TL_RT(3);
     if (wave_geometry) {  // wave-uniform
         // Wave-uniform choice of the light loop.
@@ -939,9 +959,11 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 // q2 above is not used on this path, so it is not live across pass 1); after the loop the
                 // unscaled ones once more for the finish. launder() keeps the compiler from merging the
                 // rebuilds with the computation above (which would keep q2 live across the loop: it spilled).
-                const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoFaithful, s.bal[wave_id],
+                PBR_PHASE("pass1");
+                const BalMasks bm = balanced_pass1<false>(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoFaithful, s.bal[wave_id],
                                                    s.bal_light, prof);
                 bal_items = wave_live_items(bm);
+                PBR_PHASE("invariants");
                 launder(p);
                 q2 = pair_invariants(p, ps, fast2);
                 faithful_scale(q2);
@@ -951,8 +973,11 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 #if PBR_BAL_PROFILE
                 const long long t_l1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
+                PBR_PHASE("invariants2");
                 launder(p);
-                q2 = pair_invariants(p, ps, fast2);
+                q2 = pair_finish_invariants(p, ps, fast2);  // the rare exact re-pass forms the full set itself
+                finish_q2_only = true;
+                rough2 = p.roughness;
                 pos2 = p.pos;
 #if PBR_BAL_PROFILE
                 const v2 dep = dot3(q2.n, q2.v);
@@ -976,11 +1001,13 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 #endif
             }
         } else if (faithful_wave) {
+            PBR_COLD("faithful_nonlean");
             form_q2();
             if (!CULL) faithful_scale(q2);
             d2 = lighting_fast<CULL, false, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
             if (!CULL) faithful_unscale(q2);
         } else if (lean_wave) {
+            PBR_COLD("lean_exact");
             if constexpr (BAL == 2 && !CULL) {
 #if PBR_BAL_PROFILE
                 unsigned long long* prof = s.prof[wave_id];
@@ -1002,7 +1029,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                     p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? rrow : 0, vb ? rrow + 1 : 0,
                                                       vb && gb.pairs_aligned);
                 };
-                const BalMasks bm = balanced_pass1(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoExact, s.bal[wave_id],
+                const BalMasks bm = balanced_pass1<true>(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoExact, s.bal[wave_id],
                                                    s.bal_light, prof);
                 bal_items = wave_live_items(bm);
                 q2 = pair_invariants(p, ps, fast2);
@@ -1010,17 +1037,19 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                                                              kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
                                                              prof);
                 reload();
-                q2 = pair_invariants(p, ps, fast2);
+                q2 = pair_invariants(p, ps, fast2);  // the full set: the finish-only one measured slower here (SGPRs)
                 pos2 = p.pos;
             } else {
                 form_q2();
                 d2 = lighting_fast<CULL, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
             }
         } else {
+            PBR_COLD("general");
             form_q2();
             d2 = lighting_fast<CULL, false>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
         }
     } else {
+        PBR_COLD("background");
         form_q2();  // background only: the sky pass reads N
     }
     TL_RT(4);
@@ -1032,6 +1061,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     // light loops executed for its geometry pixels: light terms evaluated (every light of the pass in the
     // uniform loop, the survivors of the wave's box under culling, the live items of the balanced lists) and
     // the balanced pass-1 back-face tests.
+    PBR_PHASE("stats_repass");
     const int n_exact = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
     const int geo_px = __popcll(lanes(ga)) + __popcll(lanes(gb_));
     if ((tid & 63) == 0 && tile_kept != nullptr) {
@@ -1050,8 +1080,15 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const long long t_b0 = (long long)__builtin_amdgcn_s_memtime();
 #endif
     if (n_exact != 0) {  // wave-uniform: rare (edge inputs, EXACT_ONLY)
+        PBR_COLD("exact_repass");
         f3 ea, eb;
-        lighting_exact_wave(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, ea, eb);
+        PixelInvariants fa = ua, fb = ub;
+        if (BAL != 0 && finish_q2_only) {  // the light-loop fields too (make_invariants' operations)
+            const PixelInvariants2 qf = complete_invariants(q2, rough2, fast2);
+            fa = unpack_invariants(qf, 0);
+            fb = unpack_invariants(qf, 1);
+        }
+        lighting_exact_wave(fa, fb, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, ea, eb);
         if (need_a) da = ea;
         if (need_b) db = eb;
     }
@@ -1069,6 +1106,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     }
 #endif
     // The output offset re-derived from the hardware ids (lane_id_fresh): same pixel as xa, y above.
+    PBR_PHASE("finish_setup");
     const int ln = lane_id_fresh();
     const int sx = blockIdx.x * kTileW + 2 * (ln & 31);
     const int64_t orow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
@@ -1092,6 +1130,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     if (lanes(ga || gb_) != 0)  // wave-uniform
         finish_pair<AMBIENT, APPLY_AO>(q2, ua, ub, ao_a, ao_b, da, db, ps, env, ok_a, ok_b, faithful_wave, ga, gb_, ca,
                                        cb);
+    PBR_PHASE("store");
     if (va && !ga) ca = sky_pixel(ua.n, ps, fr.sky, !exact_only);
     if (vb && !gb_) cb = sky_pixel(ub.n, ps, fr.sky, !exact_only);
     bool keep_a, keep_b;
@@ -1660,7 +1699,7 @@ hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels,
     PBR_BI_SWITCH(PBR_WAVE_TIMELINE) ", " PBR_BI_SWITCH(PBR_DEBUG_BOUNDS) ", " PBR_BI_SWITCH(PBR_SPLIT_BAL) ", " \
     PBR_BI_SWITCH(PBR_POW5_LDS) ", " PBR_BI_SWITCH(PBR_POW5_GLIBC_FROM) ", "                                     \
     PBR_BI_SWITCH(PBR_POW5_FAST3_GLIBC_FROM) ", " PBR_BI_SWITCH(PBR_FAITHFUL_GAMMA_LO) ", "                      \
-    PBR_BI_SWITCH(PBR_ATAN2F_KMAX)
+    PBR_BI_SWITCH(PBR_ATAN2F_KMAX) ", " PBR_BI_SWITCH(PBR_CENSUS)
 #if PBR_BAL_TU
 extern "C" __attribute__((used, visibility("default"))) const char pbr_unit_info_shade_kernels_bal[] =
     PBR_UNIT_INFO("shade_kernels_bal", PBR_KERNEL_SWITCHES);
