@@ -79,6 +79,9 @@ constexpr int kTileW = 64;  // pixels; 32 work-items x 2 pixels
 #ifndef PBR_LEAN_MIN_WAVES
 #define PBR_LEAN_MIN_WAVES 4  // waves per SIMD the culled lean pair kernel is register-allocated for
 #endif
+#ifndef PBR_LEAN_TILES
+#define PBR_LEAN_TILES 1  // development: 2 = two tiles per wave in the uniform lean kernels (shade_lean_kernel)
+#endif
 #ifndef PBR_LEAN_UNIFORM_MIN_WAVES
 #define PBR_LEAN_UNIFORM_MIN_WAVES 5  // ... and the unculled (uniform-loop) faithful or constant-ambient ones
 #endif
@@ -617,7 +620,7 @@ __device__ __forceinline__ float4 finish_lit(f3 ambient, float ao, f3 direct, co
         return make_float4(pow_inv_gamma_faithful(lit.x), pow_inv_gamma_faithful(lit.y),
                            pow_inv_gamma_faithful(lit.z), ps.opacity);
     }
-    PBR_COLD("exact_finish");
+    PBR_PHASE("xfinish");  // the exact finish (the faithful census stops here)
     lit = mk3(reinhard(lit.x, fast), reinhard(lit.y, fast), reinhard(lit.z, fast));  // Default.hlsl:153
     return make_float4(pow_inv_gamma(lit.x), pow_inv_gamma(lit.y), pow_inv_gamma(lit.z),
                        ps.opacity);
@@ -1007,7 +1010,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             d2 = lighting_fast<CULL, false, true>(q2, pos2, fast2, lights, ps, wb, cull_enabled, redo, kept_total);
             if (!CULL) faithful_unscale(q2);
         } else if (lean_wave) {
-            PBR_COLD("lean_exact");
+            PBR_PHASE("xpass1");  // the exact balanced kernel's path (the faithful census stops here)
             if constexpr (BAL == 2 && !CULL) {
 #if PBR_BAL_PROFILE
                 unsigned long long* prof = s.prof[wave_id];
@@ -1032,10 +1035,12 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 const BalMasks bm = balanced_pass1<true>(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoExact, s.bal[wave_id],
                                                    s.bal_light, prof);
                 bal_items = wave_live_items(bm);
+                PBR_PHASE("xinvariants");
                 q2 = pair_invariants(p, ps, fast2);
                 d2 = lighting_fast<false, true, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
                                                              kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
                                                              prof);
+                PBR_PHASE("xinvariants2");
                 reload();
                 q2 = pair_invariants(p, ps, fast2);  // the full set: the finish-only one measured slower here (SGPRs)
                 pos2 = p.pos;
@@ -1155,11 +1160,12 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 
 // One wave's 64x2 pixels: wave wave_id (tile rows 2 wave_id, 2 wave_id + 1) of tile (tile_x, tile_y), statistics
 // slot wave_global. The caller has staged the powf tables.
+// `pre`: the pair as the caller already loaded it (the two-tile development kernel, PBR_LEAN_TILES), else nullptr.
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, bool FAITHFUL>
 __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs& ps, const float4* __restrict__ lights,
                                           const float4* __restrict__ env, const FrameArgs& fr,
                                           int32_t* __restrict__ tile_kept, int tile_x, int tile_y, int wave_id,
-                                          int64_t wave_global) {
+                                          int64_t wave_global, const PairIn* pre = nullptr) {
     TL_BEGIN();
     const int tid = threadIdx.x;
     const int xa = tile_x * kTileW + 2 * (tid & 31);
@@ -1196,8 +1202,9 @@ __device__ __forceinline__ void lean_wave(const GBufferArgs& gb, const PassArgs&
                                                   : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
         }
-        PairIn p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
-                                                 vb && gb.pairs_aligned);
+        PairIn p = pre != nullptr ? *pre
+                                  : load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
+                                                                  vb && gb.pairs_aligned);
         TileBounds wb{};
         bool cull_enabled = false;
         FirstSurvivors first;  // the first survivor masks, for the faithful term count and the culled walk
@@ -1347,6 +1354,33 @@ __global__ __launch_bounds__(64, (lean_min_waves<AMBIENT, CULL, FAITHFUL>())) vo
     // powf tables -> LDS: the exact finish's gamma, spot cones, the faithful gamma's edges (+ atanf rows with IBL)
     load_libm_tables<AMBIENT == kAmbientIblDiffuse>();
     __syncthreads();
+#if PBR_LEAN_TILES == 2
+    // Development (PBR_LEAN_TILES=2, uniform loops): each wave shades two tiles' 64x2 pixels, tile rows 2t and 2t + 1
+    // (blockIdx.y = 4 t + wave), with the second tile's G-buffer pair loaded before the first tile is shaded, so
+    // that its loads are in flight under the first tile's light loop.
+    if constexpr (!CULL) {
+        const int wave_id = blockIdx.y & 3, ty0 = (blockIdx.y >> 2) * 2;
+        const int tiles_y = (gb.height + kTileH - 1) / kTileH;
+        auto load_tile = [&](int ty) {
+            const int xa = blockIdx.x * kTileW + 2 * (threadIdx.x & 31);
+            const int y = ty * kTileH + 2 * wave_id + (threadIdx.x >> 5);
+            const bool va = (xa < gb.width) && (y < gb.height), vb = (xa + 1 < gb.width) && (y < gb.height);
+            const int64_t row = (int64_t)y * gb.row_stride;
+            return load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? row + xa : 0, vb ? row + xa + 1 : 0,
+                                                 vb && gb.pairs_aligned);
+        };
+        const bool has1 = ty0 + 1 < tiles_y;  // uniform
+        const PairIn p0 = load_tile(ty0);
+        const PairIn p1 = load_tile(has1 ? ty0 + 1 : ty0);
+        auto slot = [&](int ty) { return ((int64_t)ty * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id; };
+        lean_wave<AMBIENT, F0_PLANE, APPLY_AO, CULL, FAITHFUL>(gb, ps, lights, env, fr, tile_kept, blockIdx.x, ty0,
+                                                               wave_id, slot(ty0), &p0);
+        if (has1)
+            lean_wave<AMBIENT, F0_PLANE, APPLY_AO, CULL, FAITHFUL>(gb, ps, lights, env, fr, tile_kept, blockIdx.x,
+                                                                   ty0 + 1, wave_id, slot(ty0 + 1), &p1);
+        return;
+    }
+#endif
     lean_wave<AMBIENT, F0_PLANE, APPLY_AO, CULL, FAITHFUL>(gb, ps, lights, env, fr, tile_kept, blockIdx.x,
                                                            blockIdx.y >> 2, blockIdx.y & 3,
                                                            ((int64_t)(blockIdx.y >> 2) * gridDim.x + blockIdx.x) *
@@ -1624,7 +1658,7 @@ static hipError_t launch_variant(const LaunchArgs& a, hipStream_t stream) {
         if (!CULL && a.ps.balanced != 0)
             return launch_balanced<AMBIENT, F0_PLANE, APPLY_AO>(a, grid, stream);
         if (a.lean) {  // uniform loops, no sky pass (shade_lean_kernel): one wave per workgroup
-            const dim3 wgrid(grid.x, grid.y * (kBlock / 64));
+            const dim3 wgrid(grid.x, (PBR_LEAN_TILES == 2 && !CULL ? (grid.y + 1) / 2 : grid.y) * (kBlock / 64));
             if (a.ps.faithful)
                 hipLaunchKernelGGL((shade_lean_kernel<AMBIENT, F0_PLANE, APPLY_AO, CULL, true>), wgrid, dim3(64), 0,
                                    stream, a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept);
@@ -1699,7 +1733,7 @@ hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels,
     PBR_BI_SWITCH(PBR_WAVE_TIMELINE) ", " PBR_BI_SWITCH(PBR_DEBUG_BOUNDS) ", " PBR_BI_SWITCH(PBR_SPLIT_BAL) ", " \
     PBR_BI_SWITCH(PBR_POW5_LDS) ", " PBR_BI_SWITCH(PBR_POW5_GLIBC_FROM) ", "                                     \
     PBR_BI_SWITCH(PBR_POW5_FAST3_GLIBC_FROM) ", " PBR_BI_SWITCH(PBR_FAITHFUL_GAMMA_LO) ", "                      \
-    PBR_BI_SWITCH(PBR_ATAN2F_KMAX) ", " PBR_BI_SWITCH(PBR_CENSUS)
+    PBR_BI_SWITCH(PBR_ATAN2F_KMAX) ", " PBR_BI_SWITCH(PBR_CENSUS) ", " PBR_BI_SWITCH(PBR_LEAN_TILES)
 #if PBR_BAL_TU
 extern "C" __attribute__((used, visibility("default"))) const char pbr_unit_info_shade_kernels_bal[] =
     PBR_UNIT_INFO("shade_kernels_bal", PBR_KERNEL_SWITCHES);

@@ -16,8 +16,8 @@ on a path from the one marker to the next without crossing another marker. Those
     lanes);
   * uniform-rare: blocks behind a wave-uniform branch (`s_cbranch_scc*` / `vcc*`) that is not the phase's main line
     (fallbacks, special-value paths): listed, not counted;
-  * cold: blocks holding IEEE-division sequences or fp64 glibc code (the rare-lane patches of the faithful kernel):
-    listed, not counted.
+  * cold: blocks holding IEEE-division sequences or fp64 glibc polynomials (FMAs: the rare-lane patches), and code
+    after a PBR_COLD marker (fallbacks and other modes' branches): not counted.
 Loops (pass 2) are weighted by their iteration count per wave (`--weights pass2=34.7`, from the balanced phase
 profile / pass statistics); every other phase runs once per wave. Classes and SIMD-cycle weights follow
 tools/isa_census_pass2.py (DESIGN.md §5's measured costs); `v_writelane` / `v_readlane` (SGPR spills to VGPR lanes and
@@ -124,8 +124,9 @@ def is_cold(b):
     ops = [op for _, op, _ in b.insns()]
     if any(op.startswith(("v_div_scale", "v_div_fmas", "v_div_fixup")) for op in ops):
         return True  # an IEEE division: the exact fallback's sequence
-    if sum(1 for op in ops if re.match(r"v_(fma|mul|add)_f64", op)) >= 3:
-        return True  # fp64 polynomial: glibc's powf / the exact x^5 patched in for rare lanes
+    if sum(1 for op in ops if re.match(r"v_fmac?_f64", op)) >= 3:
+        return True  # fp64 polynomial (FMAs): glibc's powf patched in for rare lanes (the exact x^5's plain fp64
+        # products, v_mul_f64 only, are the exact kernel's main path)
     return False
 
 
