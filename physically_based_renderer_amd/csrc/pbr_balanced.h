@@ -82,8 +82,10 @@ __device__ unsigned long long* g_bal_prof_buf;  // 16 per wave, wave = block * 4
 // sends a live pixel to the exact re-pass (at position 0 it did for every pixel within 0.01 of the origin).
 constexpr int kBalLdsStride = kBalMaxLights + 4;  // 68 floats: every array 16-byte aligned
 constexpr float kBalSentinelPos = 0x1p24f;
+// `strength_scale`: 4 for the exact balanced kernel, whose items take 4x the radiance (brdf_x2's QUARTER form; the host
+// keeps every point strength within 2^50 for it, so the product cannot overflow), 1 otherwise.
 __device__ __forceinline__ void stage_balanced_lights(const float4* __restrict__ lights, int b0, int b1,
-                                                      float* lds_lights) {
+                                                      float* lds_lights, float strength_scale = 1.0f) {
     const int t = (int)threadIdx.x;
     if (t < kBalLdsStride) {
         float4 p = make_float4(0.0f, 0.0f, 0.0f, 0.0f), st = p;
@@ -96,9 +98,9 @@ __device__ __forceinline__ void stage_balanced_lights(const float4* __restrict__
         lds_lights[0 * kBalLdsStride + t] = p.x;
         lds_lights[1 * kBalLdsStride + t] = p.y;
         lds_lights[2 * kBalLdsStride + t] = p.z;
-        lds_lights[3 * kBalLdsStride + t] = st.x;
-        lds_lights[4 * kBalLdsStride + t] = st.y;
-        lds_lights[5 * kBalLdsStride + t] = st.z;
+        lds_lights[3 * kBalLdsStride + t] = st.x * strength_scale;
+        lds_lights[4 * kBalLdsStride + t] = st.y * strength_scale;
+        lds_lights[5 * kBalLdsStride + t] = st.z * strength_scale;
     }
 }
 
@@ -200,9 +202,9 @@ __device__ __forceinline__ ItemPixel load_item(const float4* src) {
     return p;
 }
 
-// The exact (default-mode) record: the unscaled lean-loop invariants of make_invariants, less the three that
-// are one subtraction from another field (1 - F0, a^2 - 1, 1 - k: re-derived by load_item_x with the same
-// operation, so bit for bit the same values). The pixel's sum so far (its directional lights), from which the
+// The exact (default-mode) record: the lean-loop invariants of make_invariants in brdf_x2's QUARTER form (N / 4, k / 4,
+// 16 N.V: exact scalings), less the three that are one subtraction from another field (1 - F0, a^2 - 1, 1 - k:
+// re-derived by load_item_x with the same operation on the unscaled value, so bit for bit the same values). The pixel's sum so far (its directional lights), from which the
 // evaluating lane continues in the reference's order, travels separately (BalancedWaveLds::start): written by
 // the owner before the exchange, it is not held in registers through it.
 struct ItemPixelX {
@@ -216,15 +218,16 @@ __device__ __forceinline__ ItemPixelX item_pixel_x(const PixelInvariants2& q, co
                                                    uint32_t live1, int origin) {
     ItemPixelX r;
     r.pos = lane(pos, e);
-    r.n = lane(q.n, e);
+    const f3 n = lane(q.n, e);
+    r.n = mk3(0.25f * n.x, 0.25f * n.y, 0.25f * n.z);  // QUARTER
     r.v = lane(q.v, e);
     r.albedo = lane(q.albedo, e);
     r.f0 = lane(q.f0, e);
     r.omm = e ? q.one_minus_metal.y : q.one_minus_metal.x;
     r.a_sqr = e ? q.a_sqr.y : q.a_sqr.x;
-    r.k = e ? q.k.y : q.k.x;
+    r.k = 0.25f * (e ? q.k.y : q.k.x);                       // QUARTER: k / 4
     r.ggx_v = e ? q.ggx_v.y : q.ggx_v.x;
-    r.nv4 = e ? q.four_n_dot_v.y : q.four_n_dot_v.x;
+    r.nv4 = 4.0f * (e ? q.four_n_dot_v.y : q.four_n_dot_v.x);  // QUARTER: 16 N.V
     r.live0 = live0;
     r.live1 = live1;
     r.origin = origin;
@@ -264,8 +267,8 @@ __device__ __forceinline__ ItemPixelX load_item_x(const float4* src) {
     p.live1 = __float_as_uint(f.y);
     p.origin = __float_as_int(f.z);
     p.omf0 = mk3(1.0f - p.f0.x, 1.0f - p.f0.y, 1.0f - p.f0.z);  // make_invariants' operations
-    p.a2m1 = p.a_sqr - 1.0f;
-    p.omk = 1.0f - p.k;
+    p.a2m1 = 16.0f * (p.a_sqr - 1.0f);                           // QUARTER: 16 (a^2 - 1)
+    p.omk = 1.0f - 4.0f * p.k;                                   // 1 - k (4 (k / 4) is k exactly)
     return p;
 }
 template <bool EXACT>
@@ -445,7 +448,7 @@ __device__ __forceinline__ f3x2 exact_point_items2(const ItemPixelX& p, const f3
     const f3x2 h = normalize_x2(add3(q.v, l), ok);
     const v2 dsat = max_dsat(dist);
     const v2 att = recip_nr(dsat * dsat).r;
-    return brdf_x2<true>(q, f3x2{ls.x * att, ls.y * att, ls.z * att}, l, h, ok, live);
+    return brdf_x2<true, true>(q, f3x2{ls.x * att, ls.y * att, ls.z * att}, l, h, ok, live);  // ls: 4x strengths
 }
 
 // The live-light masks of the pair's pixels (pass 1), light j at bit j % 32 of word j / 32.

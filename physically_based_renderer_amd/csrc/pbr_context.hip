@@ -99,6 +99,7 @@ struct pbr_context {
     // PBR_BALANCED_MIN overrides both (0 disables).
     int balanced_min = -1;
     bool points_flag_ok = false;  // pbr_set_pass: every point light inside the fast-path window
+    bool points_quarter_ok = false;  // ... and every point strength within 2^50 (the exact balanced items' 4x radiance)
     int pixels_per_thread = 2;  // kernel layout: packed pixel pairs (measured faster); PBR_PIXELS_PER_THREAD=1 overrides
     bool lean = true;  // uniform-loop passes without a sky pass use the lean pair kernel (PBR_LEAN=0: off)
     std::string last_error;
@@ -407,6 +408,10 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
         sl.capacity = cap;
     }
     bool points_ok = true;  // every point light's fast-path flag is set (the balanced pass needs it)
+    // The exact balanced kernel's items carry 4x the radiance (pbr_balanced.h, stage_balanced_lights; brdf_x2's QUARTER
+    // form): with |strength| <= 2^50 the scaled products stay below 2^126 (term factors <= 2^57.1 x 2^13.3 attenuation
+    // x 4 x 2^50), so every scaling is exact and no term overflows where the reference's does not.
+    bool quarter_ok = true;
     if (n > 0) {
         std::memcpy(sl.h, pass->lights, sizeof(pbr_light) * (size_t)n);
         // The kernel's per-light fast-path flag travels in the unused pad1 of the uploaded copy
@@ -427,7 +432,10 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
                 if (!directional) ok = ok && std::isfinite(L.strength[k]);
             }
             L.pad1 = ok ? 1.0f : 0.0f;
-            if (i >= nd && i < nd + np) points_ok = points_ok && ok;
+            if (i >= nd && i < nd + np) {
+                points_ok = points_ok && ok;
+                for (int k = 0; k < 3; ++k) quarter_ok = quarter_ok && std::fabs(L.strength[k]) <= 0x1p50f;
+            }
         }
         e = before_write(ctx, sl.use, s, si);
         if (e != hipSuccess) return fail_hip(ctx, e, "pbr_set_pass order");
@@ -468,6 +476,7 @@ int pbr_set_pass(pbr_context* ctx, const pbr_pass_desc* pass, void* stream) {
         for (int k = 0; k < 3; ++k) nonneg = nonneg && pass->ambient_light[k] >= 0.0f;
     ctx->faithful_pass_ok = nonneg;
     ctx->points_flag_ok = points_ok;
+    ctx->points_quarter_ok = points_ok && quarter_ok;
     ctx->ambient_mode = pass->ambient_mode;
     ctx->flags = pass->flags;
     ctx->pass_set = true;
@@ -609,7 +618,7 @@ int shade(pbr_context* ctx, const pbr_gbuffer_soa* gb, const pbr_frame_desc* fr,
                         a.ps.n_spot == 0 && a.ps.n_point >= bal_min && a.ps.n_point <= pbr::kBalMaxLights;
     a.ps.balanced = !bal_ok                                                ? 0
                     : a.ps.faithful == 1                                   ? 1
-                    : a.ps.faithful == 0 && !a.exact_only && a.ps.n_dir == 0 ? 2
+                    : a.ps.faithful == 0 && !a.exact_only && a.ps.n_dir == 0 && ctx->points_quarter_ok ? 2
                                                                            : 0;
 
     DeviceGuard g(ctx->device);

@@ -187,7 +187,8 @@ __device__ __forceinline__ v2 pow5_light(v2 x, uint64_t live = ~0ull) {
     const double dx = (double)x.x, dy = (double)x.y;
     const double dx2 = dx * dx, dy2 = dy * dy;
     v2 p = v2{(float)(dx2 * dx2 * dx), (float)(dy2 * dy2 * dy)};
-    if (__builtin_expect((lanes(x.x > PBR_POW5_GLIBC_FROM || x.y > PBR_POW5_GLIBC_FROM) & live) != 0, 0)) {
+    // Two ballots of the compares themselves: a ballot of their || was formed through a VGPR (v_cndmask, v_cmp_ne).
+    if (__builtin_expect(((lanes(x.x > PBR_POW5_GLIBC_FROM) | lanes(x.y > PBR_POW5_GLIBC_FROM)) & live) != 0, 0)) {
         if (x.x > PBR_POW5_GLIBC_FROM && on(live)) p.x = pow5_glibc(x.x);
         if (x.y > PBR_POW5_GLIBC_FROM && on(live)) p.y = pow5_glibc(x.y);
     }
@@ -301,16 +302,23 @@ __device__ __forceinline__ v2 div_pi(v2 x) { return vfma(x, splat(kInvPiHi), x *
 //    near F0 or an exact cancellation (a multiple of ulp(F0)/2 >= 2^-45), so F is 0 or >= 2^-45 and
 //    ndf_g F stays inside the division window for any p: the p == 0 / p >= 2^-40 test is moot.
 //
-template <bool LEAN>
+// QUARTER (lean only; the exact wave-balanced items, pbr_balanced.h): q carries N / 4, k / 4 (1 - k as it is),
+// 16 (a^2 - 1), 16 N.V in place of 4 N.V, and `radiance` is 4x the reference's -- all exact power-of-two scalings, so
+// max(N.H, 0) / 4 and max(N.L, 0) / 4 come out of the dots bit for bit (every product of them is 0 or >= 2^-110 in
+// the window) and below 1 in lean waves, where they ride on the dot's clamp bit instead of a v_max per element; the
+// quarters cancel against the scaled invariants in every later operation (N.H^2 / 16 x 16 (a^2 - 1); N.L / 4 over
+// N.L (1 - k) / 4 + k / 4; 16 N.V x N.L / 4; 4 radiance x N.L / 4), so each value is the unscaled loop's bit for bit.
+template <bool LEAN, bool QUARTER = false>
 __device__ __forceinline__ f3x2 brdf_x2(const PixelInvariants2& q, f3x2 radiance, f3x2 l, f3x2 h, m2& ok,
                                         uint64_t live = ~0ull) {
-    v2 n_dot_h = vmax(dot3(q.n, h), splat(0.0f));
+    static_assert(LEAN || !QUARTER, "the clamp form needs the lean bounds |N|, |H|, |L| <= 1 + 2^-19");
+    v2 n_dot_h = QUARTER ? dot3_sat(q.n, h) : vmax(dot3(q.n, h), splat(0.0f));
     v2 n_dot_h_sqr = n_dot_h * n_dot_h;
     v2 den = (n_dot_h_sqr * q.a_sqr_minus_1 + 1.0f);
     den = kPi * den * den;
     if (!LEAN) ok &= ge(den, 0x1p-60f) & le(den, 0x1p60f);
     v2 ndf = div_nr(q.a_sqr, recip_nr(den));
-    v2 n_dot_l = vmax(dot3(q.n, l), splat(0.0f));
+    v2 n_dot_l = QUARTER ? dot3_sat(q.n, l) : vmax(dot3(q.n, l), splat(0.0f));
     v2 ggx_l = div_nr(n_dot_l, recip_nr(n_dot_l * q.one_minus_k + q.k));
     v2 g = ggx_l * q.ggx_v;
     v2 cos_theta = dot3_sat(h, q.v);

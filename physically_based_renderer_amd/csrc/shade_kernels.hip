@@ -863,7 +863,8 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     if ((threadIdx.x & 63) < 16) bal_prof[threadIdx.x & 63] = 0;
 #endif
     load_libm_tables<AMBIENT == kAmbientIblDiffuse>();  // powf (+ atanf with IBL) tables -> LDS (pbr_device_math.h)
-    if constexpr (BAL != 0) stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light);
+    if constexpr (BAL != 0)
+        stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light, BAL == 2 ? 4.0f : 1.0f);
     __syncthreads();
     PBR_PHASE("load_window");
 

@@ -272,6 +272,31 @@ def test_balanced_range_cut_in_pass1(mode, ctx_pair, gpu):
     check_mode(mode, got, want, ref)
 
 
+@pytest.mark.parametrize("top", [2.0 ** 50, 2.0 ** 51, 1.0e30])
+def test_balanced_exact_strength_bound(top, ctx_pair, gpu):
+    """The exact balanced items run brdf_x2's QUARTER form (N / 4, k / 4, 16 (a^2 - 1), 16 N.V, 4x strengths: exact
+    power-of-two scalings, pbr_balanced.h), whose 4x radiance the host bounds: every point strength within 2^50
+    (pbr_context.hip, points_quarter_ok), else the uniform exact loop. Strengths spanning 2^-20 .. `top` (one light
+    at `top`, others over 20 decades): bit-identical to the uniform loop and the oracle either way, and the balanced
+    kernel runs exactly when the bound holds."""
+    rng = np.random.default_rng(71)
+    nl = 24
+    planes, lights = _scene(rng, 256, 8, nl)
+    lights[:, 0:3] = (10.0 ** rng.uniform(-6, 14, (nl, 3))).astype(np.float32)
+    lights[3, 0:3] = (top, 1.0, 2.0 ** -20)
+    pc = PassConstants(num_point_lights=nl, lights_array=lights, flags=0)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc)
+    kernel = bal.last_kernel()
+    want, redo_p = run(plain, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    print(f"strengths up to {top:g}: {kernel}, redo {redo_b} vs {redo_p}")
+    assert kernel.endswith(", 2>") == (top <= 2.0 ** 50)
+    assert redo_b <= redo_p
+    check_mode("exact", got, want, ref)
+
+
 def test_balanced_light_outside_window_sends_all_to_exact(ctx_pair, gpu):
     """A light whose position is outside the fast-path window (|x| > 2^20): every pixel is redone exactly,
     as in the uniform loop (frames bit-identical to the oracle there)."""
