@@ -277,13 +277,14 @@ def test_balanced_exact_strength_bound(top, ctx_pair, gpu):
     """The exact balanced items run brdf_x2's QUARTER form (N / 4, k / 4, 16 (a^2 - 1), 16 N.V, 4x strengths: exact
     power-of-two scalings, pbr_balanced.h), whose 4x radiance the host bounds: every point strength within 2^50
     (pbr_context.hip, points_quarter_ok), else the uniform exact loop. Strengths spanning 2^-20 .. `top` (one light
-    at `top`, others over 20 decades): bit-identical to the uniform loop and the oracle either way, and the balanced
-    kernel runs exactly when the bound holds."""
+    at `top`, one negative, others over 20 decades): bit-identical to the uniform loop and the oracle either way, and
+    the balanced kernel runs exactly when the bound holds."""
     rng = np.random.default_rng(71)
     nl = 24
     planes, lights = _scene(rng, 256, 8, nl)
     lights[:, 0:3] = (10.0 ** rng.uniform(-6, 14, (nl, 3))).astype(np.float32)
     lights[3, 0:3] = (top, 1.0, 2.0 ** -20)
+    lights[7, 0:3] = (-5.0e3, 0.0, -2.0 ** -30)  # negative and zero strengths scale exactly too
     pc = PassConstants(num_point_lights=nl, lights_array=lights, flags=0)
     gb = GBuffer.from_host(planes, gpu)
     bal, plain = ctx_pair
