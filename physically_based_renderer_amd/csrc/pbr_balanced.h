@@ -107,14 +107,11 @@ __device__ __forceinline__ void stage_balanced_lights(const float4* __restrict__
 constexpr int kBalRecX = 6;        // float4 per exchanged pixel record, exact passes
 
 struct BalancedWaveLds {
-    float4 rec[64 * kBalRec];  // 7 KiB
+    float4 rec[64 * kBalRec];  // 7 KiB: the exchanged records; then each evaluating lane's two results (float4 0, 1)
     union {
         int hist[64];          // ranking
-        int flag[128];         // pass 2 results: the pixel stayed inside the fast-path window, by origin
+        int2 rank[64];         // by owner lane: the ranks of its two pixels (pass 2 -> hand-back)
     };
-    // By origin: exact passes, each pixel's sum before its point lights (written by the owner); then the
-    // pixel's result (written by the evaluating lane once the pixel is done, after it has read the start).
-    float start[3][128];
 };
 
 // The per-pixel loop invariants of the faithful scaled lean loop (the scalar view of PixelInvariants2 after
@@ -651,6 +648,8 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     w.hist[lane_id] = incl - h;  // exclusive prefix: first rank of each bin
     wave_lds_sync();
     const int rank_a = w.hist[bin_a] + pos_a, rank_b = w.hist[bin_b] + pos_b;
+    wave_lds_sync();
+    w.rank[lane_id] = make_int2(rank_a, rank_b);  // read back at the hand-back (nothing of it lives through pass 2)
     // rank r < 64 -> lane r, first pixel; r >= 64 -> lane 127 - r, second pixel.
     using Item = std::conditional_t<EXACT, ItemPixelX, ItemPixel>;
     Item ia, ib;
@@ -685,20 +684,32 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     f3 accx = mk3(0.0f, 0.0f, 0.0f);
     uint64_t fail = 0, second = 0;
     uint64_t m = ((uint64_t)cur.live1 << 32) | cur.live0;
-    // A finished pixel's result goes to LDS at once (its start slot, read already, and its flag), so that nothing
-    // of it stays in registers: for the first pixel before the second one's iterations, for the second before the
-    // sentinel iterations that wait for the wave's other lanes.
-    auto put_result = [&]() {  // divergent: the lanes whose current pixel is done
+    // A finished pixel's result (its three sums and whether it stayed inside the fast-path window) goes to LDS at
+    // once, so that nothing of it stays in registers: into the evaluating lane's own record slot, float4 0 for its
+    // first pixel and 1 for its second -- the slot held the lane's second record, which the lane has read before it
+    // writes there (a wave's LDS operations execute in order); the owner finds it from the pixel's rank.
+    auto result = [&]() {  // divergent: the lanes whose current pixel is done
         const f3 r = EXACT ? accx : mk3(acc.x.x + acc.x.y, acc.y.x + acc.y.y, acc.z.x + acc.z.y);
-        const int o = PBR_BOUNDS(cur.origin, 128, kBoundsLds);
-        w.start[0][o] = r.x;
-        w.start[1][o] = r.y;
-        w.start[2][o] = r.z;
-        w.flag[o] = on(fail) ? 0 : 1;
+        return make_float4(r.x, r.y, r.z, on(fail) ? 0.0f : 1.0f);
     };
-    auto next_pixel = [&]() {  // divergent: the lanes whose first pixel is done
+    // Two dwords at a time from wherever they sit (ds_write2_b32, as store_item): as a float4 store the compiler
+    // first assembled the quad in consecutive registers.
+    const uint32_t slot_addr = lds_addr(&w.rec[R * lane_id]);
+    auto put_result = [&](int k, float4 v) {
+        if (k == 0) {
+            lds_write2<0>(slot_addr, v.x, v.y);
+            lds_write2<2>(slot_addr, v.z, v.w);
+        } else {
+            lds_write2<4>(slot_addr, v.x, v.y);
+            lds_write2<6>(slot_addr, v.z, v.w);
+        }
+    };
+    // The lanes whose first pixel is done (divergent): read the second record, then hand the first result to the slot
+    // it came from (the sums are still in acc / accx), then start the second pixel's sums.
+    auto next_pixel = [&]() {
         cur = load_item_any<EXACT>(&w.rec[R * lane_id]);
         m = ((uint64_t)cur.live1 << 32) | cur.live0;
+        put_result(0, result());
         acc = splat3(0.0f, 0.0f, 0.0f);
         accx = mk3(0.0f, 0.0f, 0.0f);
     };
@@ -707,15 +718,12 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     // mask is empty, formed by ONE compare per iteration (at its end: the next iteration's live lanes are the rest).
     uint64_t zero = lanes(m == 0);
     if (zero != 0) {  // uniform
-        if (on(zero)) {
-            put_result();
-            next_pixel();
-        }
+        if (on(zero)) next_pixel();
         second = zero;
         const uint64_t first_done = zero;
         zero = lanes(m == 0);
         const uint64_t empty = first_done & zero;
-        if (empty != 0 && on(empty)) put_result();
+        if (empty != 0 && on(empty)) put_result(1, result());
     }
 #if PBR_BAL_PROFILE
     int iters = 0;
@@ -749,7 +757,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
             const uint64_t done = zero & live;
             if (done != 0) {  // uniform
                 if (on(done)) {
-                    put_result();
+                    if (on(second)) put_result(1, result());
                     if (!on(second)) next_pixel();
                 }
                 fail &= ~done;
@@ -759,7 +767,7 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
                     zero = lanes(m == 0);
                     // A second pixel with no live light: hand it back now (rare).
                     const uint64_t empty = first_done & zero;
-                    if (empty != 0 && on(empty)) put_result();
+                    if (empty != 0 && on(empty)) put_result(1, result());
                 }
             }
             live = ~zero & exec;
@@ -767,18 +775,21 @@ __device__ __forceinline__ void lighting_balanced_points(const PixelInvariants2&
     }
     BAL_PROF_T(t3);
     PBR_PHASE("handback");
-    // ---- hand the results back: the owner reads its two pixels' (by origin 2 lane + element)
+    // ---- hand the results back: the owner reads its two pixels' from their evaluating lanes' slots (rank r < 64:
+    // lane r, first pixel; r >= 64: lane 127 - r, second pixel)
     wave_lds_sync();
-    const float2 rx = reinterpret_cast<const float2*>(w.start[0])[lane_id];
-    const float2 ry = reinterpret_cast<const float2*>(w.start[1])[lane_id];
-    const float2 rz = reinterpret_cast<const float2*>(w.start[2])[lane_id];
-    const int2 fl = reinterpret_cast<const int2*>(w.flag)[lane_id];
+    const int2 rk = w.rank[lane_id];
+    auto slot = [&](int r) {
+        r = PBR_BOUNDS(r, 128, kBoundsLds);
+        return r < 64 ? R * r : R * (127 - r) + 1;
+    };
+    const float4 ra = w.rec[slot(rk.x)], rb = w.rec[slot(rk.y)];
     wave_lds_sync();
     if constexpr (EXACT)
-        sum = f3x2{v2{rx.x, rx.y}, v2{ry.x, ry.y}, v2{rz.x, rz.y}};
+        sum = f3x2{v2{ra.x, rb.x}, v2{ra.y, rb.y}, v2{ra.z, rb.z}};
     else
-        sum = f3x2{sum.x + v2{rx.x, rx.y}, sum.y + v2{ry.x, ry.y}, sum.z + v2{rz.x, rz.y}};
-    redo |= mask2(live_a && fl.x == 0, live_b && fl.y == 0);
+        sum = f3x2{sum.x + v2{ra.x, rb.x}, sum.y + v2{ra.y, rb.y}, sum.z + v2{ra.z, rb.z}};
+    redo |= mask2(live_a && ra.w == 0.0f, live_b && rb.w == 0.0f);
 #if PBR_BAL_PROFILE
     BAL_PROF_T(t4);
     BAL_PROF_ADD(1, t2 - t1);

@@ -24,8 +24,27 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 TICK_NS = 10.0  # s_memrealtime: 100 MHz
 
 
+def block_idle(tl: np.ndarray, waves_per_block: int = 4) -> dict:
+    """Multi-wave workgroups (the tile kernel: 4 waves, one per SIMD; row = block * 4 + wave): a workgroup's LDS is
+    released when its last wave ends, and with LDS-limited occupancy no new workgroup starts on the CU before that,
+    so each wave's slot idles from its own end to its workgroup's last end. Returns that idle time as a fraction of
+    the waves' lifetimes, and the spread of the waves' lifetimes inside a workgroup."""
+    n = (len(tl) // waves_per_block) * waves_per_block
+    t = tl[:n, 1:6].astype(np.int64).reshape(-1, waves_per_block, 5)
+    ok = (t[:, :, 0] != 0).all(axis=1)
+    t = t[ok] * TICK_NS / 1e3
+    entry, done = t[:, :, 0], t[:, :, 4]
+    life = done - entry
+    idle = done.max(axis=1, keepdims=True) - done
+    return {"blocks": int(ok.sum()), "idle_over_life": round(float(idle.sum() / life.sum()), 4),
+            "idle_us_mean_per_wave": round(float(idle.mean()), 3),
+            "life_spread_in_block_us_mean": round(float((life.max(axis=1) - life.min(axis=1)).mean()), 3),
+            "entry_spread_in_block_us_mean": round(float((entry.max(axis=1) - entry.min(axis=1)).mean()), 3)}
+
+
 def analyse(tl: np.ndarray, name: str) -> dict:
     """tl: (waves, 8) uint64 stamps of one launch (rows of waves that never ran are zero)."""
+    blk = block_idle(tl)
     tl = tl[tl[:, 1] != 0]
     hw, xcc = (tl[:, 0] & 0xFFFFFFFF).astype(np.int64), ((tl[:, 0] >> 32) & 0xFFFF).astype(np.int64)
     flags = (tl[:, 0] >> 48).astype(np.int64)  # shade_lean_kernel: 1 = pixels re-passed, 2 = not a faithful wave
@@ -58,6 +77,7 @@ def analyse(tl: np.ndarray, name: str) -> dict:
     waves_per_simd = np.bincount(np.unique(simd, return_inverse=True)[1])
     out = {
         "workload": name, "waves": int(len(tl)), "simds": int(n_simd), "launch_us": round(float(end), 2),
+        "block_idle": blk,
         "waves_per_simd": {"mean": round(float(waves_per_simd.mean()), 2), "min": int(waves_per_simd.min()),
                            "max": int(waves_per_simd.max())},
         "mean_resident_waves_per_simd": round(float(resid), 3),
