@@ -83,11 +83,12 @@ __device__ unsigned long long* g_bal_prof_buf;  // 16 per wave, wave = block * 4
 constexpr int kBalLdsStride = kBalMaxLights + 4;  // 68 floats: every array 16-byte aligned
 constexpr float kBalSentinelPos = 0x1p24f;
 // `strength_scale`: 4 for the exact balanced kernel, whose items take 4x the radiance (brdf_x2's QUARTER form; the host
-// keeps every point strength within 2^50 for it, so the product cannot overflow), 1 otherwise.
+// keeps every point strength within 2^50 for it, so the product cannot overflow), 1 otherwise. NT: the
+// workgroup's work-items (64 in one-wave workgroups: two rounds for the 68 entries).
+template <int NT = 256>
 __device__ __forceinline__ void stage_balanced_lights(const float4* __restrict__ lights, int b0, int b1,
                                                       float* lds_lights, float strength_scale = 1.0f) {
-    const int t = (int)threadIdx.x;
-    if (t < kBalLdsStride) {
+    for (int t = (int)threadIdx.x; t < kBalLdsStride; t += NT) {
         float4 p = make_float4(0.0f, 0.0f, 0.0f, 0.0f), st = p;
         if (t < b1 - b0) {
             p = lights[3 * (b0 + t) + 2];

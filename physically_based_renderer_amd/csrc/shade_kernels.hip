@@ -76,6 +76,9 @@ constexpr int kTileW = 64;  // pixels; 32 work-items x 2 pixels
 #ifndef PBR_X2_MIN_WAVES
 #define PBR_X2_MIN_WAVES 4  // waves per SIMD the packed kernel is register-allocated for
 #endif
+#ifndef PBR_BAL_WAVES
+#define PBR_BAL_WAVES 4  // waves per workgroup of the balanced-list kernels: 4 (one tile) or 1 (one wave of a tile)
+#endif
 #ifndef PBR_LEAN_MIN_WAVES
 #define PBR_LEAN_MIN_WAVES 4  // waves per SIMD the culled lean pair kernel is register-allocated for
 #endif
@@ -124,6 +127,16 @@ struct Lds {
 #endif
     int kept_sum, geo_waves;  // tiled-culling statistics of the block
     int exact_px;             // pixels of the block the exact path redid
+};
+
+// The one-wave workgroups of the balanced kernels (PBR_BAL_WAVES == 1): the wave's exchange region and the pass's
+// point lights only (9.3 KiB + the libm tables: 16 workgroups fit a CU's LDS).
+struct LdsBal1 {
+    BalancedWaveLds bal[1];
+    float bal_light[6 * kBalLdsStride];
+#if PBR_BAL_PROFILE
+    unsigned long long prof[1][16];
+#endif
 };
 
 // Stage lights [begin, begin+count) of the global list into LDS, culled against the tile when CULL.
@@ -847,14 +860,14 @@ __device__ __forceinline__ void repass_exact(const GBufferArgs& gb, const PassAr
 
 // BAL (untiled only; PassArgs::balanced): the variant whose lean waves take the wave-balanced point-light lists
 // (pbr_balanced.h) -- 1: faithful passes, 2: exact passes; separate instantiations so that the other variants'
-// register allocation is untouched.
+// register allocation is untouched. With PBR_BAL_WAVES == 1 the balanced variants run one wave per workgroup
+// (blockIdx.y = 4 * tile row + wave, as shade_lean_kernel), each staging the lights itself.
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO, bool CULL, int BAL = 0>
-__global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GBufferArgs gb, PassArgs ps,
-                                                            const float4* __restrict__ lights,
-                                                            const float4* __restrict__ env, FrameArgs fr,
-                                                            int32_t* __restrict__ tile_kept,
-                                                            bool exact_only) {
-    __shared__ Lds s;
+__global__ __launch_bounds__(BAL != 0 && PBR_BAL_WAVES == 1 ? 64 : kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(
+    GBufferArgs gb, PassArgs ps, const float4* __restrict__ lights, const float4* __restrict__ env, FrameArgs fr,
+    int32_t* __restrict__ tile_kept, bool exact_only) {
+    constexpr bool kOneWave = BAL != 0 && PBR_BAL_WAVES == 1;
+    __shared__ std::conditional_t<kOneWave, LdsBal1, Lds> s;
     TL_BEGIN();
     PBR_PHASE("entry");
 #if PBR_BAL_PROFILE
@@ -864,14 +877,18 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 #endif
     load_libm_tables<AMBIENT == kAmbientIblDiffuse>();  // powf (+ atanf with IBL) tables -> LDS (pbr_device_math.h)
     if constexpr (BAL != 0)
-        stage_balanced_lights(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light, BAL == 2 ? 4.0f : 1.0f);
+        stage_balanced_lights<kOneWave ? 64 : kBlock>(lights, ps.n_dir, ps.n_dir + ps.n_point, s.bal_light,
+                                                      BAL == 2 ? 4.0f : 1.0f);
     __syncthreads();
     PBR_PHASE("load_window");
 
-    const int tid = threadIdx.x;
-    const int wave_id = __builtin_amdgcn_readfirstlane(tid) >> 6;  // wave-uniform (SGPR)
+    // wave_id: the wave's two rows of the tile (wave-uniform, SGPR); wslot: its exchange region in this workgroup.
+    const int wave_id = kOneWave ? (int)(blockIdx.y & 3) : __builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
+    const int wslot = kOneWave ? 0 : wave_id;
+    const int tile_y = kOneWave ? (int)(blockIdx.y >> 2) : (int)blockIdx.y;
+    const int tid = kOneWave ? 64 * wave_id + (int)threadIdx.x : (int)threadIdx.x;
     const int xa = blockIdx.x * kTileW + 2 * (tid & 31);
-    const int y = blockIdx.y * kTileH + (tid >> 5);
+    const int y = tile_y * kTileH + (tid >> 5);
     const bool va = (xa < gb.width) && (y < gb.height);
     const bool vb = (xa + 1 < gb.width) && (y < gb.height);
     const int64_t row = (int64_t)y * gb.row_stride;
@@ -927,8 +944,6 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     f3x2 pos2 = p.pos;
     f3x2 d2 = splat3(0.0f, 0.0f, 0.0f);
     bool faithful_wave = false;  // wave-uniform: the faithful loop ran, so the finish may be faithful too
-    bool finish_q2_only = false;  // wave-uniform: q2 holds only the finish's fields (the wave-balanced paths)
-    v2 rough2 = splat(0.0f);      // ... and then the pair's roughness, for the exact re-pass's full set
     TL_RT(3);
     if (wave_geometry) {  // wave-uniform
         // Wave-uniform choice of the light loop.
@@ -955,7 +970,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             if constexpr (BAL == 1 && !CULL) {
 #if PBR_BAL_PROFILE
                 BAL_PROF_ADD(7, (long long)__builtin_amdgcn_s_memtime() - t_entry);
-                unsigned long long* prof = s.prof[wave_id];
+                unsigned long long* prof = s.prof[wslot];
 #else
                 unsigned long long* prof = nullptr;
 #endif
@@ -964,7 +979,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 // unscaled ones once more for the finish. launder() keeps the compiler from merging the
                 // rebuilds with the computation above (which would keep q2 live across the loop: it spilled).
                 PBR_PHASE("pass1");
-                const BalMasks bm = balanced_pass1<false>(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoFaithful, s.bal[wave_id],
+                const BalMasks bm = balanced_pass1<false>(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoFaithful, s.bal[wslot],
                                                    s.bal_light, prof);
                 bal_items = wave_live_items(bm);
                 PBR_PHASE("invariants");
@@ -972,16 +987,14 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                 q2 = pair_invariants(p, ps, fast2);
                 faithful_scale(q2);
                 d2 = lighting_fast<false, true, true, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
-                                                            kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
+                                                            kept_total, &s.bal[wslot], s.bal_light, ga, gb_, bm,
                                                             prof);
 #if PBR_BAL_PROFILE
                 const long long t_l1 = (long long)__builtin_amdgcn_s_memtime();
 #endif
                 PBR_PHASE("invariants2");
                 launder(p);
-                q2 = pair_finish_invariants(p, ps, fast2);  // the rare exact re-pass forms the full set itself
-                finish_q2_only = true;
-                rough2 = p.roughness;
+                q2 = pair_finish_invariants(p, ps, fast2);  // the rare exact re-pass reads its pixels again
                 pos2 = p.pos;
 #if PBR_BAL_PROFILE
                 const v2 dep = dot3(q2.n, q2.v);
@@ -1014,7 +1027,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
             PBR_PHASE("xpass1");  // the exact balanced kernel's path (the faithful census stops here)
             if constexpr (BAL == 2 && !CULL) {
 #if PBR_BAL_PROFILE
-                unsigned long long* prof = s.prof[wave_id];
+                unsigned long long* prof = s.prof[wslot];
 #else
                 unsigned long long* prof = nullptr;
 #endif
@@ -1028,18 +1041,18 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
                     asm volatile("" ::: "memory");
                     const int rl = lane_id_fresh();
                     const int rx = blockIdx.x * kTileW + 2 * (rl & 31);
-                    const int ry = blockIdx.y * kTileH + 2 * wave_id + (rl >> 5);
+                    const int ry = tile_y * kTileH + 2 * wave_id + (rl >> 5);
                     const int64_t rrow = (int64_t)ry * gb.row_stride + rx;
                     p = load_pair<F0_PLANE, APPLY_AO>(gb, ps, va ? rrow : 0, vb ? rrow + 1 : 0,
                                                       vb && gb.pairs_aligned);
                 };
-                const BalMasks bm = balanced_pass1<true>(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoExact, s.bal[wave_id],
+                const BalMasks bm = balanced_pass1<true>(p.pos, p.n, ga, gb_, ps.n_point, kBalDistLoExact, s.bal[wslot],
                                                    s.bal_light, prof);
                 bal_items = wave_live_items(bm);
                 PBR_PHASE("xinvariants");
                 q2 = pair_invariants(p, ps, fast2);
                 d2 = lighting_fast<false, true, false, true>(q2, p.pos, fast2, lights, ps, wb, cull_enabled, redo,
-                                                             kept_total, &s.bal[wave_id], s.bal_light, ga, gb_, bm,
+                                                             kept_total, &s.bal[wslot], s.bal_light, ga, gb_, bm,
                                                              prof);
                 PBR_PHASE("xinvariants2");
                 reload();
@@ -1071,7 +1084,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     const int n_exact = __popcll(lanes(need_a)) + __popcll(lanes(need_b));
     const int geo_px = __popcll(lanes(ga)) + __popcll(lanes(gb_));
     if ((tid & 63) == 0 && tile_kept != nullptr) {
-        const int64_t slot = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
+        const int64_t slot = ((int64_t)tile_y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
         const int n_ps = CULL ? kept_total : ps.n_point + ps.n_spot;
         const int terms = !wave_geometry ? 0 : bal_items >= 0 ? bal_items + ps.n_dir * geo_px : (ps.n_dir + n_ps) * geo_px;
         int32_t* st = tile_kept + kStatsPerBlock * slot;
@@ -1085,16 +1098,13 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
 #if PBR_BAL_PROFILE
     const long long t_b0 = (long long)__builtin_amdgcn_s_memtime();
 #endif
-    if (n_exact != 0) {  // wave-uniform: rare (edge inputs, EXACT_ONLY)
+    // The balanced variants re-pass their pixels after the stores (repass_exact, as shade_lean_kernel): up to
+    // kLanesRepassMax pixels one at a time with the lanes splitting the lights, instead of every light for the
+    // whole wave here (~50 us for one pixel, which made the few waves that have one the launch's last).
+    if (BAL == 0 && n_exact != 0) {  // wave-uniform: rare (edge inputs, EXACT_ONLY)
         PBR_COLD("exact_repass");
         f3 ea, eb;
-        PixelInvariants fa = ua, fb = ub;
-        if (BAL != 0 && finish_q2_only) {  // the light-loop fields too (make_invariants' operations)
-            const PixelInvariants2 qf = complete_invariants(q2, rough2, fast2);
-            fa = unpack_invariants(qf, 0);
-            fb = unpack_invariants(qf, 1);
-        }
-        lighting_exact_wave(fa, fb, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, ea, eb);
+        lighting_exact_wave(ua, ub, lane(pos2, 0), lane(pos2, 1), need_a, need_b, lights, ps, ea, eb);
         if (need_a) da = ea;
         if (need_b) db = eb;
     }
@@ -1107,7 +1117,7 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const int l = threadIdx.x & 63;
-        const int64_t wv = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
+        const int64_t wv = ((int64_t)tile_y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id;
         if (l < 16 && g_bal_prof_buf != nullptr && wv < (int64_t)(1 << 18)) g_bal_prof_buf[wv * 16 + l] += bal_prof[l];
     }
 #endif
@@ -1115,12 +1125,12 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
     PBR_PHASE("finish_setup");
     const int ln = lane_id_fresh();
     const int sx = blockIdx.x * kTileW + 2 * (ln & 31);
-    const int64_t orow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
+    const int64_t orow = (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * fr.out_stride + sx;
     // PBR_FLAG_APPLY_AO: the AO pair is read only now, for the finish (Default.hlsl:150 ambient * AO): a value
     // loaded at entry would be live across the light loops (it was the one spilled value of the AO kernels).
     float ao_a = 1.0f, ao_b = 1.0f;
     if (APPLY_AO) {
-        const int64_t arow = (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
+        const int64_t arow = (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx;
         if (vb && gb.pairs_aligned) {
             const float2 t = *reinterpret_cast<const float2*>(
                 gb.plane[11] + PBR_BOUNDS_PIXEL(arow, gb.width, gb.height, gb.row_stride, 2, kBoundsGBuffer));
@@ -1133,18 +1143,22 @@ __global__ __launch_bounds__(kBlock, PBR_X2_MIN_WAVES) void shade_tile_kernel(GB
         }
     }
     float4 ca = make_float4(0.0f, 0.0f, 0.0f, 0.0f), cb = ca;
-    if (lanes(ga || gb_) != 0)  // wave-uniform
-        finish_pair<AMBIENT, APPLY_AO>(q2, ua, ub, ao_a, ao_b, da, db, ps, env, ok_a, ok_b, faithful_wave, ga, gb_, ca,
-                                       cb);
+    const bool live_a = ga && !(BAL != 0 && need_a), live_b = gb_ && !(BAL != 0 && need_b);
+    if (lanes(live_a || live_b) != 0)  // wave-uniform
+        finish_pair<AMBIENT, APPLY_AO>(q2, ua, ub, ao_a, ao_b, da, db, ps, env, ok_a, ok_b, faithful_wave, live_a,
+                                       live_b, ca, cb);
     PBR_PHASE("store");
     if (va && !ga) ca = sky_pixel(ua.n, ps, fr.sky, !exact_only);
     if (vb && !gb_) cb = sky_pixel(ub.n, ps, fr.sky, !exact_only);
     bool keep_a, keep_b;
-    alpha_keep_pair(gb, (int64_t)(blockIdx.y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx, ga, gb_, ca,
+    alpha_keep_pair(gb, (int64_t)(tile_y * kTileH + 2 * wave_id + (ln >> 5)) * gb.row_stride + sx, ga, gb_, ca,
                     cb, keep_a, keep_b);
-    if (va && keep_a) store_pixel(fr, orow, ca);
-    if (vb && keep_b) store_pixel(fr, orow + 1, cb);
-    TL_END(((long long)blockIdx.y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id);
+    if (va && keep_a && !(BAL != 0 && need_a)) store_pixel(fr, orow, ca);
+    if (vb && keep_b && !(BAL != 0 && need_b)) store_pixel(fr, orow + 1, cb);
+    if (BAL != 0 && n_exact != 0)  // wave-uniform
+        repass_exact<AMBIENT, F0_PLANE, APPLY_AO>(gb, ps, lights, env, fr, blockIdx.x, tile_y, wave_id, need_a, need_b,
+                                                  n_exact, faithful_wave);
+    TL_END(((long long)tile_y * gridDim.x + blockIdx.x) * (kBlock / 64) + wave_id);
 }
 
 // ---- Lean pair kernel ------------------------------------------------------------------------------------------
@@ -1552,12 +1566,14 @@ hipError_t launch_balanced(const LaunchArgs& a, dim3 grid, hipStream_t stream);
 #if PBR_BAL_TU == PBR_SPLIT_BAL
 template <int AMBIENT, bool F0_PLANE, bool APPLY_AO>
 hipError_t launch_balanced(const LaunchArgs& a, dim3 grid, hipStream_t stream) {
+    const dim3 g = PBR_BAL_WAVES == 1 ? dim3(grid.x, grid.y * (kBlock / 64)) : grid;
+    const dim3 blk(PBR_BAL_WAVES == 1 ? 64 : kBlock);
     if (a.ps.balanced == 1)
-        hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 1>), grid, dim3(kBlock), 0, stream,
-                           a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
+        hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 1>), g, blk, 0, stream, a.gb, a.ps,
+                           a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
     else
-        hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 2>), grid, dim3(kBlock), 0, stream,
-                           a.gb, a.ps, a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
+        hipLaunchKernelGGL((shade_tile_kernel<AMBIENT, F0_PLANE, APPLY_AO, false, 2>), g, blk, 0, stream, a.gb, a.ps,
+                           a.lights, a.env, a.frame, a.tile_kept, a.exact_only);
     return hipGetLastError();
 }
 #define PBR_INSTANTIATE_BAL(A, F, O) template hipError_t launch_balanced<A, F, O>(const LaunchArgs&, dim3, hipStream_t);
@@ -1734,7 +1750,8 @@ hipError_t launch_decode_unorm16(const uint16_t* src, float4* dst, int n_texels,
     PBR_BI_SWITCH(PBR_WAVE_TIMELINE) ", " PBR_BI_SWITCH(PBR_DEBUG_BOUNDS) ", " PBR_BI_SWITCH(PBR_SPLIT_BAL) ", " \
     PBR_BI_SWITCH(PBR_POW5_LDS) ", " PBR_BI_SWITCH(PBR_POW5_GLIBC_FROM) ", "                                     \
     PBR_BI_SWITCH(PBR_POW5_FAST3_GLIBC_FROM) ", " PBR_BI_SWITCH(PBR_FAITHFUL_GAMMA_LO) ", "                      \
-    PBR_BI_SWITCH(PBR_ATAN2F_KMAX) ", " PBR_BI_SWITCH(PBR_CENSUS) ", " PBR_BI_SWITCH(PBR_LEAN_TILES)
+    PBR_BI_SWITCH(PBR_ATAN2F_KMAX) ", " PBR_BI_SWITCH(PBR_CENSUS) ", " PBR_BI_SWITCH(PBR_LEAN_TILES) ", "    \
+    PBR_BI_SWITCH(PBR_BAL_WAVES)
 #if PBR_BAL_TU
 extern "C" __attribute__((used, visibility("default"))) const char pbr_unit_info_shade_kernels_bal[] =
     PBR_UNIT_INFO("shade_kernels_bal", PBR_KERNEL_SWITCHES);
