@@ -313,6 +313,38 @@ def test_balanced_light_outside_window_sends_all_to_exact(ctx_pair, gpu):
     assert close(got, want)
 
 
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("n_on_light", [1, 3, 8, 9, 20, 64])
+def test_balanced_repass_after_stores(n_on_light, mode, ctx_pair, gpu):
+    """The balanced kernels re-pass their exact pixels after the wave's stores (shade_kernels.hip, repass_exact):
+    up to kLanesRepassMax (8) pixels one at a time with the lanes splitting the lights, more with every lane
+    taking its own pixels. Pixels placed exactly on a light (the reference's L = 0 / 0: NaN, absorbed by the
+    maxNum clamps; the balanced pass's distance window sends them to the re-pass) in one wave of 128 pixels, the
+    other waves of the frame untouched: the re-passed pixels, the pixels around them that the wave stored first
+    and the redo count all as the uniform loop and the oracle have them."""
+    rng = np.random.default_rng(300 + n_on_light)
+    w, h, nl = 128, 8, 64
+    planes, lights = _scene(rng, w, h, nl)
+    # wave 1 of tile 0 covers rows 2-3, columns 0-63 (64 lanes x 2 pixels): put n pixels of it on lights
+    cols = rng.permutation(64 * 2)[:n_on_light]
+    for i, c in enumerate(cols):
+        x, y = int(c % 64), 2 + int(c // 64)
+        planes[0:3, y, x] = lights[i % nl, 8:11]
+    flags = N.PBR_FLAG_FAITHFUL if mode == "faithful" else 0
+    pc = PassConstants(num_point_lights=nl, lights_array=lights, flags=flags)
+    gb = GBuffer.from_host(planes, gpu)
+    bal, plain = ctx_pair
+    got, redo_b = run(bal, gb, pc)
+    assert ", false, 1>" in bal.last_kernel() or ", false, 2>" in bal.last_kernel(), bal.last_kernel()
+    want, redo_p = run(plain, gb, pc)
+    ref = O.shade(list(planes), oracle_pass_from_constants(pc), pc.light_array(), None, n_threads=4)
+    print(f"repass ({mode}, {n_on_light} on lights): redo {redo_b} vs {redo_p}, kernel {bal.last_kernel()}")
+    assert redo_b >= n_on_light  # every pixel on a light is redone (the rest of the scene stays in the window)
+    assert redo_b <= redo_p
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    check_mode(mode, got, want, ref)
+
+
 @pytest.fixture(scope="module")
 def ctx_default(gpu):
     """A context with the built-in per-mode minimums (PBR_BALANCED_MIN unset)."""
